@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""bench.py -- all-pairs AJI matrix fill on MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1: launched by torch.distributed.run, one rank per GPU)
+
+Workload (BASELINE.json metric "10k-genome all-vs-all"): a synthetic
+10,000-genome x 100-SCP database (SURVEY.md §8d SYN generator, seed
+20250213), all-vs-all AJI.  Every rank generates the same DB (deterministic),
+loads it into HBM once (pfaai_load), and owns a contiguous block of output
+rows balanced by pair count.  One step = the hot path over the resident
+inputs: work-list build (the reference's E construction, without E) + the
+scatter/Jaccard/AJI row kernel for the rank's rows, then (N > 1) an RCCL
+gather of the rows' fp64 AJI blocks to rank 0.  Total work is fixed as N
+grows: scaling "strong".  value = genome pairs of the whole matrix / max
+step time over ranks.
+
+Extra JSON objects:
+  roofline      dominant kernel k_rows: algorithmic bytes per launch
+                (8 B per E event + 8 B per AJI written) / its mean
+                duration from HIP events on the launch stream over the timed
+                region; peak 8 TB/s HBM; traffic from the committed rocprofv3
+                PMC summary (profiles/) when present.
+  cpu_baseline  the reference CLI (oracle/_ref/par_fastaai.x, built from its
+                own sources) on a bounded SYN sample, rank 0 at N = 1 only;
+                falls back to the CPU oracle ("port") if the binary is absent.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (first: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
+
+
+def log(msg):
+    print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def split_rows(n, world):
+    """Contiguous row blocks of the upper triangle with ~equal pairs
+    (row a owns n-1-a pairs)."""
+    before = lambda a: a * n - a * (a + 1) // 2  # pairs in rows < a  # noqa: E731
+    total = n * (n - 1) // 2
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r // world
+        lo, hi = cuts[-1], n
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if before(mid) < target:
+                lo = mid + 1
+            else:
+                hi = mid
+        cuts.append(lo)
+    cuts.append(n)
+    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+
+
+def traffic_from_profiles():
+    """HBM bytes per k_rows launch from profiles/pmc_k_rows.json (written by
+    tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes)."""
+    p = os.path.join(ROOT, "profiles", "pmc_k_rows.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(sample_genomes=320, n_prot=100):
+    """Reference CLI on a SYN sample; returns the cpu_baseline object."""
+    from parfastaai_amd import syn
+
+    ref = os.path.join(ROOT, "oracle", "_ref", "par_fastaai.x")
+    threads = min(16, os.cpu_count() or 1)
+    pairs = sample_genomes * (sample_genomes - 1) // 2
+    if os.path.exists(ref):
+        with tempfile.TemporaryDirectory() as td:
+            db = os.path.join(td, "syn.db")
+            syn.write_db(db, sample_genomes, n_prot)
+            env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+            t0 = time.perf_counter()
+            r = subprocess.run([ref, db, os.path.join(td, "out.csv")], capture_output=True, text=True, env=env,
+                               timeout=600)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0:
+                raise RuntimeError(f"reference exited {r.returncode}")
+
+            def ms(label):
+                m = re.search(re.escape(label) + r"\s*:\s*([0-9.e+]+) ms", r.stdout)
+                return float(m.group(1)) if m else None
+
+            e_ms, jac_ms = ms("E constr.   (fin)"), ms("JAC Construction")
+            hot_s = (e_ms + jac_ms) / 1e3
+            return {"value": pairs / hot_s, "unit": "genome-pairs/s", "cores": threads, "kind": "reference",
+                    "sample": f"reference par_fastaai.x (built from its sources) on SYN N={sample_genomes} "
+                              f"P={n_prot} all-vs-all; hot path = its own 'E constr. (fin)' + 'JAC "
+                              f"Construction' timers = {hot_s:.2f} s (wall incl. SQLite+CSV {wall:.1f} s); "
+                              f"OMP_NUM_THREADS={threads}"}
+    # fallback: the CPU oracle (single thread restatement of the reference)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from parfastaai_amd.datastruct import ParFAAIData
+
+    g = syn.generate(sample_genomes, n_prot)
+    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    t0 = time.perf_counter()
+    O.Problem(ds.problem()).ref_run()
+    dt = time.perf_counter() - t0
+    return {"value": pairs / dt, "unit": "genome-pairs/s", "cores": 1, "kind": "port",
+            "sample": f"CPU oracle (E build + radix sort + extents + JAC) on SYN N={sample_genomes} P={n_prot}, "
+                      f"{dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--genomes", type=int, default=10000)
+    ap.add_argument("--prot", type=int, default=100)
+    ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
+    ap.add_argument("--cpu-sample", type=int, default=320)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from parfastaai_amd import _capi, syn
+    from parfastaai_amd.datastruct import ParFAAIData
+
+    t0 = time.perf_counter()
+    g = syn.generate(args.genomes, args.prot)
+    n_f = len(g["F_genome"])
+    log(f"generated SYN N={args.genomes} P={args.prot} |F|={n_f} in {time.perf_counter() - t0:.1f}s")
+    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    eng = _capi.Engine(local)
+    t0 = time.perf_counter()
+    eng.load(**ds.problem())
+    del g
+    log(f"pfaai_load (H2D + sizing) {time.perf_counter() - t0:.1f}s")
+    n_rows, n_pairs = eng.shape()
+    blocks = split_rows(n_rows, world)
+    spans = [eng.row_span(rb, re) for rb, re in blocks]
+    rb, re = blocks[rank]
+    first, count = spans[rank]
+    maxcount = max(c for _, c in spans)
+    out = torch.zeros(max(maxcount, 1), dtype=torch.float64, device=dev)
+    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+    base = out.data_ptr() - first * 8  # pfaai_run indexes by the global JAC index
+
+    def step():
+        eng.run(rb, re, 0, base, stream=stream.cuda_stream)
+        if world > 1:
+            dist.gather(out, gather, dst=0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    eng.timing(reset=True)
+    n_events = eng.stats()["n_events"]  # per run, rank-local
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    n_runs, ms_build, ms_rows = eng.timing(reset=True)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ev = torch.tensor([n_events], dtype=torch.int64, device=dev)
+        dist.all_reduce(ev)
+        total_events = int(ev.item())
+        km = torch.tensor([ms_rows / max(n_runs, 1), ms_build / max(n_runs, 1)], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        k_rows_ms_max, k_build_ms_max = km.tolist()
+    else:
+        total_events = n_events
+        k_rows_ms_max = ms_rows / max(n_runs, 1)
+        k_build_ms_max = ms_build / max(n_runs, 1)
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    if rank == 0:
+        # spot-check the gathered / local result for sanity (cheap properties)
+        if world > 1:
+            vals = torch.cat([gather[r][: spans[r][1]] for r in range(world)])
+        else:
+            vals = out[:count]
+        vmin, vmax = float(vals.min().item()), float(vals.max().item())
+        assert vals.numel() == n_pairs and 0.0 <= vmin and vmax <= 1.0, (vals.numel(), vmin, vmax)
+
+        k_rows_ms = ms_rows / max(n_runs, 1)  # rank 0's own k_rows launch duration
+        rank_pairs = count
+        alg_bytes = 8 * n_events + 8 * rank_pairs
+        achieved = alg_bytes / (k_rows_ms * 1e-3) / 1e9
+        step_bytes = 8 * total_events + 4 * n_f + 8 * n_pairs  # SURVEY §8d B_alg
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(),
+                    "kernel": "pfaai::k_rows (scatter + Jaccard + AJI)",
+                    "kernel_ms": round(k_rows_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                    "build_kernels_ms": round(ms_build / max(n_runs, 1), 4)}
+        cpu = None
+        if args.cpu_baseline != "none" and world == 1:
+            try:
+                log("cpu baseline ...")
+                cpu = cpu_baseline(args.cpu_sample, args.prot)
+            except Exception as e:  # reported, never fatal
+                cpu = {"value": None, "error": str(e)}
+        line = {
+            "metric": METRIC,
+            "value": round(n_pairs / (ms_per_step * 1e-3), 1),
+            "unit": "genome-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "i32+f64",
+            "data": "synthetic",
+            "config": {"workload": f"SYN all-vs-all N={args.genomes} P={args.prot} (BASELINE configs[2] DB; "
+                                   f"row-block sharded, RCCL gather to rank 0)",
+                       "genomes": args.genomes, "proteins": args.prot, "pairs": n_pairs, "F": n_f,
+                       "events": total_events, "parallelism": f"rowblock{world}",
+                       "hot_path_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                       "k_rows_ms_max_rank": round(k_rows_ms_max, 4),
+                       "k_build_ms_max_rank": round(k_build_ms_max, 4)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,152 @@
+/*
+ * pfaai_hip.h -- C ABI of libpfaai_hip.so, the MI355X-native all-pairs
+ * Average Jaccard Index (AJI) engine (HIP, gfx950).
+ *
+ * This is the drop-in boundary for ParFastAAI's hot path.  The reference has
+ * no FFI: its boundary is a header-only C++ template contract
+ *   producer  DataStructInterface   include/pfaai/interface.hpp:200-328
+ *   consumer  ParFAAIImpl           include/pfaai/algorithm_impl.hpp:38-357
+ * and every entry point below replaces one piece of that contract (cited per
+ * function).  Plain C types only: pointers, sizes, int codes.  The C++
+ * adapter with the ParFAAIImpl surface (run/computeJAC/computeAJI/getJAC/
+ * getAJI) is include/pfaai_hip.hpp; the Python mirror is parfastaai_amd/.
+ *
+ * Conventions
+ *   - return 0 on success; 1..3 are the reference's PFAAI_ERROR_CODE values
+ *     (interface.hpp:39-44), 4..7 are new (HIP runtime, device OOM, RCCL,
+ *     invalid argument).  pfaai_last_error() gives a message.
+ *   - host inputs are borrowed for the duration of the call; device buffers
+ *     are owned by the context; outputs are caller-owned.
+ *   - one host thread drives one context; a context owns one device.
+ */
+#ifndef PFAAI_HIP_H
+#define PFAAI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFAAI_ABI_VERSION 1
+#define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
+
+/* Error codes: 0..3 mirror PFAAI_ERROR_CODE (interface.hpp:39-44). */
+enum {
+    PFAAI_OK = 0,
+    PFAAI_ERR_SQLITE_DB = 1,
+    PFAAI_ERR_SQLITE_MEM_ALLOC = 2,
+    PFAAI_ERR_CONSTRUCT = 3,
+    PFAAI_ERR_HIP = 4,
+    PFAAI_ERR_OOM = 5,
+    PFAAI_ERR_RCCL = 6,
+    PFAAI_ERR_INVALID = 7
+};
+
+/* Modes: which genome pairs are valid and how they index the JAC array.
+ *   ALL  = ParFAAIData        (ds_impl.hpp:38-151)   pairs a<b
+ *   QSUB = ParFAAIQSubData    (ds_impl.hpp:158-337)  -q query subset
+ *   QT   = ParFAAIQryTgtData  (ds_impl.hpp:343-490)  -r query DB vs target DB */
+enum { PFAAI_MODE_ALL = 0, PFAAI_MODE_QSUB = 1, PFAAI_MODE_QT = 2 };
+
+/* Run flags */
+#define PFAAI_FLAG_REF_COMPAT 1u /* reproduce reference quirks */
+#define PFAAI_FLAG_EMIT_JAC 2u   /* also write the JAC S (f64) and N (i32) */
+
+typedef struct pfaai_ctx pfaai_ctx;
+
+/*
+ * The data-structure view the reference's DataStructInterface exposes
+ * (refLp/refF/refT, interface.hpp:246-250) plus the mode's index maps
+ * (isQryGenome/isValidPair/genomePairToIndex, interface.hpp:276-293).
+ * F is ordered by (tetramer, protein, genome): block t = [Lp[t], Lp[t+1]).
+ */
+typedef struct {
+    int32_t mode;          /* PFAAI_MODE_* */
+    int32_t n_ids;         /* genome ids used in F (QT: n_tgt + n_qry; query ids offset by n_tgt) */
+    int32_t n_prot;        /* P */
+    int32_t t_cols;        /* columns of T (T is P x t_cols, row-major) */
+    int32_t n_qry;         /* QSUB: |query list|; QT: genomes of the query DB */
+    int32_t n_tgt;         /* QSUB: n_ids - n_qry; QT: genomes of the target DB; ALL: unused */
+    int64_t n_f;           /* |F| (must be < 2^31) */
+    const int64_t* Lp;     /* [PFAAI_NTETRAMERS + 1] exclusive prefix of Lc, Lp[160000] = n_f */
+    const int32_t* F_prot; /* [n_f] F[i].first  (protein index) */
+    const int32_t* F_genome; /* [n_f] F[i].second (genome id) */
+    const int32_t* T;      /* [n_prot * t_cols] T(p, g) tetramer counts */
+    const uint8_t* is_q;   /* [n_ids] QSUB/QT: 1 for query genomes (NULL for ALL) */
+    const int32_t* q_index; /* [n_ids] QSUB: position of the genome in the query file, -1 otherwise */
+    const int32_t* t_rank; /* [n_ids] QSUB: rank among the non-query genomes, -1 otherwise */
+} pfaai_problem;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int pfaai_version(void);
+int pfaai_create(pfaai_ctx** ctx, int device_id);
+int pfaai_destroy(pfaai_ctx* ctx);
+const char* pfaai_last_error(const pfaai_ctx* ctx);
+
+/* Copy a problem to the device and keep it resident (replaces the reference
+ * handing ParFAAIImpl const refs to Lc/Lp/F/T, algorithm_impl.hpp:50-55,
+ * 75-79).  Replaces any previously loaded problem. */
+int pfaai_load(pfaai_ctx* ctx, const pfaai_problem* prob);
+
+/* Number of output rows (ALL: n_ids; QSUB/QT: n_qry) and of JAC pairs
+ * (nGenomePairs: ds_impl.hpp:78-80, 244-249, 406). */
+int pfaai_shape(const pfaai_ctx* ctx, int64_t* n_rows, int64_t* n_pairs);
+
+/* JAC-index span [first, first+count) written by rows [row_begin, row_end).
+ * Rows map to contiguous spans in ALL and QT; in QSUB each row has two
+ * segments (cross block, triangle block) and the span is their hull. */
+int pfaai_row_span(const pfaai_ctx* ctx, int64_t row_begin, int64_t row_end,
+                   int64_t* first, int64_t* count);
+
+/*
+ * Device-resident hot path for output rows [row_begin, row_end):
+ *   E construction (ds_helper.hpp:206-421) -> per-(row,protein) work lists,
+ *   pair-expansion scatter of intersection counts (no E, no sort),
+ *   Jaccard normalisation + protein-ordered fp64 S/N reduction
+ *   (algorithm_impl.hpp:222-306), AJI = S/N (algorithm_impl.hpp:309-322).
+ * d_aji / d_S / d_N are DEVICE pointers to arrays indexed by the full JAC
+ * index (length n_pairs); only the rows' entries are written.  d_aji may be
+ * NULL (then only S/N), d_S/d_N are required with PFAAI_FLAG_EMIT_JAC.
+ * stream: a hipStream_t (NULL = the context's own stream).  Asynchronous.
+ */
+int pfaai_run(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
+              double* d_aji, double* d_S, int32_t* d_N, void* stream);
+
+/* Synchronous convenience: all rows, results copied into HOST arrays of
+ * length n_pairs (any may be NULL).  The ParFAAIImpl::run() equivalent
+ * (algorithm_impl.hpp:325-329). */
+int pfaai_compute(pfaai_ctx* ctx, uint32_t flags, double* h_aji, double* h_S,
+                  int32_t* h_N);
+
+/* |E| of the last run, counted by the scatter kernel (equals the reference's
+ * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and
+ * device times (ms) of its two phases: work-list build, row kernel.
+ * Valid after the run's stream has been synchronised. */
+int pfaai_last_stats(pfaai_ctx* ctx, int64_t* n_events, float* ms_build,
+                     float* ms_rows);
+
+/* Accumulated device times of every pfaai_run since the last reset: number
+ * of runs and the summed ms of the work-list build and of the row kernel
+ * (HIP events on the run's stream).  Synchronises on those events; reset != 0
+ * starts a new accumulation window afterwards. */
+int pfaai_timing(pfaai_ctx* ctx, int reset, int32_t* n_runs, double* ms_build,
+                 double* ms_rows);
+
+/* Debug materialiser for integer parity: intersection counts c(p, a, b) of
+ * output row `row` for every protein, written to a HOST array
+ * counts[p * n_ids + b] (int32, n_prot x n_ids).  Equals the run-lengths of
+ * the reference's sorted E (ds_helper.hpp:414-418) restricted to genomeA. */
+int pfaai_debug_row_counts(pfaai_ctx* ctx, int64_t row, int32_t* h_counts);
+
+/* Device memory helpers (so callers without a GPU framework can run the
+ * device-resident path): allocate/free on the context's device, copy. */
+int pfaai_device_alloc(pfaai_ctx* ctx, void** ptr, int64_t bytes);
+int pfaai_device_free(pfaai_ctx* ctx, void* ptr);
+int pfaai_memcpy_d2h(pfaai_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int pfaai_synchronize(pfaai_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFAAI_HIP_H */

@@ -1,0 +1,202 @@
+"""ctypes binding of libpfaai_hip.so (include/pfaai_hip.h).
+
+This is the only way the Python mirror reaches the engine: every compute
+call goes through the C ABI into the HIP kernels.  There is no CPU
+fallback -- if the library is missing or no GPU is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+try:  # one HIP runtime per process: torch's bundled libamdhip64 must win
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the binding
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PFAAI_HIP_LIB", os.path.join(_HERE, "lib", "libpfaai_hip.so"))
+
+NTETRAMERS = 160000
+PFAAI_OK = 0
+ERR_NAMES = {1: "SQLITE_DB", 2: "SQLITE_MEM_ALLOC", 3: "CONSTRUCT", 4: "HIP", 5: "OOM", 6: "RCCL", 7: "INVALID"}
+MODE_ALL, MODE_QSUB, MODE_QT = 0, 1, 2
+FLAG_REF_COMPAT = 1
+FLAG_EMIT_JAC = 2
+
+# every symbol include/pfaai_hip.h declares
+EXPORTS = [
+    "pfaai_version", "pfaai_create", "pfaai_destroy", "pfaai_last_error", "pfaai_load",
+    "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
+    "pfaai_debug_row_counts", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
+    "pfaai_synchronize", "pfaai_timing",
+]
+
+
+class PfaaiError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"pfaai error {code} ({ERR_NAMES.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Problem(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32), ("n_ids", ctypes.c_int32), ("n_prot", ctypes.c_int32),
+        ("t_cols", ctypes.c_int32), ("n_qry", ctypes.c_int32), ("n_tgt", ctypes.c_int32),
+        ("n_f", ctypes.c_int64),
+        ("Lp", ctypes.c_void_p), ("F_prot", ctypes.c_void_p), ("F_genome", ctypes.c_void_p),
+        ("T", ctypes.c_void_p), ("is_q", ctypes.c_void_p), ("q_index", ctypes.c_void_p),
+        ("t_rank", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def load_library():
+    """Load libpfaai_hip.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libpfaai_hip.so not found at {LIB_PATH}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    sig = {
+        "pfaai_version": (ctypes.c_int, []),
+        "pfaai_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
+        "pfaai_destroy": (ctypes.c_int, [vp]),
+        "pfaai_last_error": (ctypes.c_char_p, [vp]),
+        "pfaai_load": (ctypes.c_int, [vp, ctypes.POINTER(Problem)]),
+        "pfaai_shape": (ctypes.c_int, [vp, P64, P64]),
+        "pfaai_row_span": (ctypes.c_int, [vp, i64, i64, P64, P64]),
+        "pfaai_run": (ctypes.c_int, [vp, i64, i64, u32, vp, vp, vp, vp]),
+        "pfaai_compute": (ctypes.c_int, [vp, u32, vp, vp, vp]),
+        "pfaai_last_stats": (ctypes.c_int, [vp, P64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+        "pfaai_debug_row_counts": (ctypes.c_int, [vp, i64, vp]),
+        "pfaai_device_alloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), i64]),
+        "pfaai_device_free": (ctypes.c_int, [vp, vp]),
+        "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
+        "pfaai_synchronize": (ctypes.c_int, [vp]),
+        "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Engine:
+    """One pfaai_ctx = one device.  Owns the device-resident problem."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.pfaai_create(ctypes.byref(self.ctx), int(device))
+        if rc != PFAAI_OK:
+            raise PfaaiError(rc, f"pfaai_create(device={device}) failed (no visible GPU?)")
+        self._keep = None
+
+    def _check(self, rc, what):
+        if rc != PFAAI_OK:
+            msg = self.lib.pfaai_last_error(self.ctx)
+            raise PfaaiError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.pfaai_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- problem ----------------------------------------------------------------
+    def load(self, *, mode, n_ids, n_prot, Lp, F_prot, F_genome, T, n_qry=0, n_tgt=0,
+             is_q=None, q_index=None, t_rank=None):
+        Lp = np.ascontiguousarray(Lp, dtype=np.int64)
+        F_prot = np.ascontiguousarray(F_prot, dtype=np.int32)
+        F_genome = np.ascontiguousarray(F_genome, dtype=np.int32)
+        T = np.ascontiguousarray(T, dtype=np.int32)
+        is_q = None if is_q is None else np.ascontiguousarray(is_q, dtype=np.uint8)
+        q_index = None if q_index is None else np.ascontiguousarray(q_index, dtype=np.int32)
+        t_rank = None if t_rank is None else np.ascontiguousarray(t_rank, dtype=np.int32)
+        assert Lp.shape == (NTETRAMERS + 1,)
+        assert T.ndim == 2 and T.shape[0] == n_prot
+        pb = Problem(mode=mode, n_ids=n_ids, n_prot=n_prot, t_cols=T.shape[1], n_qry=n_qry,
+                     n_tgt=n_tgt, n_f=F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
+                     F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
+                     t_rank=_ptr(t_rank))
+        self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
+
+    def shape(self):
+        r, p = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.pfaai_shape(self.ctx, ctypes.byref(r), ctypes.byref(p)), "pfaai_shape")
+        return r.value, p.value
+
+    def row_span(self, row_begin, row_end):
+        f, c = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.pfaai_row_span(self.ctx, row_begin, row_end, ctypes.byref(f), ctypes.byref(c)),
+                    "pfaai_row_span")
+        return f.value, c.value
+
+    # -- compute ------------------------------------------------------------------
+    def compute(self, flags: int = 0):
+        """All rows; returns host (aji, S, N) in JAC-index order."""
+        _, np_ = self.shape()
+        aji = np.empty(np_, dtype=np.float64)
+        S = np.empty(np_, dtype=np.float64)
+        N = np.empty(np_, dtype=np.int32)
+        self._check(self.lib.pfaai_compute(self.ctx, flags, _ptr(aji), _ptr(S), _ptr(N)), "pfaai_compute")
+        return aji, S, N
+
+    def run(self, row_begin, row_end, flags, d_aji, d_S=None, d_N=None, stream=None):
+        """Device-resident run; d_* are device pointers (ints), stream a hipStream_t (int)."""
+        self._check(self.lib.pfaai_run(self.ctx, row_begin, row_end, flags, d_aji, d_S, d_N, stream),
+                    "pfaai_run")
+
+    def stats(self):
+        ne, mb, mr = ctypes.c_int64(), ctypes.c_float(), ctypes.c_float()
+        self._check(self.lib.pfaai_last_stats(self.ctx, ctypes.byref(ne), ctypes.byref(mb), ctypes.byref(mr)),
+                    "pfaai_last_stats")
+        return {"n_events": ne.value, "ms_build": mb.value, "ms_rows": mr.value}
+
+    def timing(self, reset=True):
+        """(n_runs, ms_build_total, ms_rows_total) of the runs since the last reset."""
+        n, b, r = ctypes.c_int32(), ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.pfaai_timing(self.ctx, int(reset), ctypes.byref(n), ctypes.byref(b), ctypes.byref(r)),
+                    "pfaai_timing")
+        return n.value, b.value, r.value
+
+    def debug_row_counts(self, row, n_prot, n_ids):
+        out = np.zeros((n_prot, n_ids), dtype=np.int32)
+        self._check(self.lib.pfaai_debug_row_counts(self.ctx, row, _ptr(out)), "pfaai_debug_row_counts")
+        return out
+
+    def synchronize(self):
+        self._check(self.lib.pfaai_synchronize(self.ctx), "pfaai_synchronize")
+
+    # -- raw device buffers (callers without a GPU framework) ---------------------
+    def alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        self._check(self.lib.pfaai_device_alloc(self.ctx, ctypes.byref(p), int(nbytes)), "pfaai_device_alloc")
+        return p.value
+
+    def free(self, ptr: int):
+        self._check(self.lib.pfaai_device_free(self.ctx, ptr), "pfaai_device_free")
+
+    def d2h(self, ptr: int, count: int, dtype) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        self._check(self.lib.pfaai_memcpy_d2h(self.ctx, _ptr(out), ptr, out.nbytes), "pfaai_memcpy_d2h")
+        return out

@@ -1,0 +1,583 @@
+// pfaai_hip.hip -- C-ABI implementation of libpfaai_hip.so (include/pfaai_hip.h).
+//
+// Owns one device per context: the problem (Lp, F, T, mode maps) stays
+// resident in HBM after pfaai_load(); pfaai_run() is stream-ordered device
+// work only (no host sync, no allocation): K-W work-list build, then K-S+J.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pfaai_hip.h"
+#include "pfaai_kernels.hpp"
+
+using namespace pfaai;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct pfaai_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool loaded = false;
+
+    // problem (host copies of scalars + small maps)
+    pfaai_problem prob{};
+    int64_t n_rows = 0, n_pairs = 0;
+    std::vector<int32_t> row_genome_h;
+    std::vector<int32_t> q_index_h;
+    int32_t max_cols = 0;
+
+    // device-resident problem
+    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col;
+    Dev dev{};
+
+    // work space
+    DevBuf cnt, rowptr, cursor, recs, sums, scalars, out_aji, out_S, out_N, dbg;
+    uint64_t recs_cap = 0;  // records needed by the whole problem (all rows)
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    bool timed = false;
+    // per-run event triples for pfaai_timing (pool reused after each reset)
+    std::vector<hipEvent_t> pool;
+    size_t pool_used = 0;
+};
+
+namespace {
+
+// scalars buffer layout (u64 each)
+enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_N = 4 };
+
+int fail(pfaai_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(pfaai_ctx* c, hipError_t e, const char* what) {
+    if (e == hipErrorOutOfMemory)
+        return fail(c, PFAAI_ERR_OOM, std::string(what) + ": " + hipGetErrorString(e));
+    return fail(c, PFAAI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, call)                                  \
+    do {                                                   \
+        hipError_t e_ = (call);                            \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+    } while (0)
+
+int ensure(pfaai_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return PFAAI_OK;
+    if (b.p) {
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    if (bytes == 0) bytes = 8;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc");
+    b.bytes = bytes;
+    return PFAAI_OK;
+}
+
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+template <typename T>
+int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
+    int rc = ensure(c, b, n * sizeof(T));
+    if (rc) return rc;
+    if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return PFAAI_OK;
+}
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Work-list build for rows [rb, re): counts, exclusive scan, fill.
+template <int MODE>
+int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool first_event) {
+    const int64_t n = (re - rb) * c->prob.n_prot;
+    auto* cnt = static_cast<uint32_t*>(c->cnt.p);
+    auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
+    auto* cursor = static_cast<unsigned long long*>(c->cursor.p);
+    auto* sums = static_cast<unsigned long long*>(c->sums.p);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    HIPCHK(c, hipMemsetAsync(cnt, 0, n * sizeof(uint32_t), s));
+    const int grid = kNTetramers;  // one workgroup per tetramer block
+    hipLaunchKernelGGL((k_tetra_records<MODE, 0>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
+                       cnt, nullptr, nullptr, nullptr, err);
+    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kScanTile));
+    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kScanThreads), 0, s, cnt, n, rowptr, sums);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, s, sums, tiles, sc + SC_GRAND);
+    hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, s, rowptr, n, sums, sc + SC_GRAND,
+                       cursor);
+    hipLaunchKernelGGL((k_tetra_records<MODE, 1>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
+                       nullptr, cursor, static_cast<uint2*>(c->recs.p), nullptr, err);
+    if (first_event) {
+        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL((k_tetra_records<MODE, 2>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
+                           nullptr, nullptr, nullptr, sc + SC_FIRST_KEY, err);
+    }
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_OK;
+}
+
+int pick_kw(int32_t max_cols) {
+    static const int kws[] = {1, 2, 3, 4, 5, 6, 8, 10};
+    const int64_t words = ceil_div(std::max<int32_t>(max_cols, 1), 2);
+    for (int kw : kws)
+        if (words <= (int64_t)kw * kRowThreads) return kw;
+    return 10;  // wider rows are split into column chunks
+}
+
+template <int MODE, int KW>
+void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t nchunks, uint32_t flags,
+                    double* aji, double* S, int32_t* N, hipStream_t s) {
+    const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    hipLaunchKernelGGL((k_rows<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                       static_cast<const unsigned long long*>(c->rowptr.p),
+                       static_cast<const uint2*>(c->recs.p), chunk, flags, sc + SC_FIRST_KEY, aji, S, N,
+                       sc + SC_EVENTS);
+}
+
+template <int MODE>
+void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S,
+                 int32_t* N, hipStream_t s) {
+    const int kw = pick_kw(c->max_cols);
+    const int32_t chunk = 2 * kw * kRowThreads;
+    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
+    switch (kw) {
+#define KCASE(K) \
+    case K: launch_rows_kw<MODE, K>(c, rb, re, chunk, nchunks, flags, aji, S, N, s); break;
+        KCASE(1) KCASE(2) KCASE(3) KCASE(4) KCASE(5) KCASE(6) KCASE(8) KCASE(10)
+#undef KCASE
+        default: break;
+    }
+}
+
+template <int MODE>
+int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+             hipStream_t s) {
+    const bool compat = flags & PFAAI_FLAG_REF_COMPAT;
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    HIPCHK(c, hipMemsetAsync(sc + SC_EVENTS, 0, sizeof(unsigned long long), s));
+    // three events per run: start, after work-list build, after row kernel
+    while (c->pool.size() < c->pool_used + 3) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->pool.push_back(e);
+    }
+    hipEvent_t* ev = &c->pool[c->pool_used];
+    c->pool_used += 3;
+    c->ev0 = ev[0];
+    c->ev1 = ev[1];
+    c->ev2 = ev[2];
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    int rc = build_records<MODE>(c, rb, re, s, compat);
+    if (rc) return rc;
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev2, s));
+    return PFAAI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfaai_version(void) { return PFAAI_ABI_VERSION; }
+
+int pfaai_create(pfaai_ctx** out, int device_id) {
+    if (!out) return PFAAI_ERR_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PFAAI_ERR_HIP;
+    if (device_id < 0 || device_id >= ndev) return PFAAI_ERR_INVALID;
+    auto* c = new pfaai_ctx();
+    c->device = device_id;
+    if (hipSetDevice(device_id) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PFAAI_ERR_HIP;
+    }
+    int rc = ensure(c, c->scalars, SC_N * sizeof(unsigned long long));
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    (void)hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long));
+    *out = c;
+    return PFAAI_OK;
+}
+
+int pfaai_destroy(pfaai_ctx* c) {
+    if (!c) return PFAAI_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->cnt, &c->rowptr, &c->cursor,
+                      &c->recs, &c->sums, &c->scalars, &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
+        release(*b);
+    for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return PFAAI_OK;
+}
+
+const char* pfaai_last_error(const pfaai_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
+    if (!c || !pb) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    c->loaded = false;
+    const pfaai_problem& p = *pb;
+    if (p.mode < 0 || p.mode > 2) return fail(c, PFAAI_ERR_INVALID, "mode must be 0, 1 or 2");
+    if (p.n_ids < 2 || p.n_prot < 1 || p.n_prot >= kMaxRuns || p.t_cols < 1)
+        return fail(c, PFAAI_ERR_INVALID, "bad sizes (n_ids >= 2, 1 <= n_prot < 4096)");
+    if (p.n_ids >= (1 << 21) || p.n_f < 0 || p.n_f >= (int64_t)1 << 31)
+        return fail(c, PFAAI_ERR_INVALID, "n_ids must be < 2^21 and |F| < 2^31");
+    if (!p.Lp || !p.F_prot || !p.F_genome || !p.T)
+        return fail(c, PFAAI_ERR_INVALID, "Lp, F_prot, F_genome and T are required");
+    if (p.Lp[0] != 0 || p.Lp[PFAAI_NTETRAMERS] != p.n_f)
+        return fail(c, PFAAI_ERR_INVALID, "Lp must start at 0 and end at n_f");
+    if (p.mode != PFAAI_MODE_ALL && !p.is_q)
+        return fail(c, PFAAI_ERR_INVALID, "is_q is required for QSUB/QT");
+    if (p.mode == PFAAI_MODE_QSUB && (!p.q_index || !p.t_rank))
+        return fail(c, PFAAI_ERR_INVALID, "q_index and t_rank are required for QSUB");
+    if (p.mode == PFAAI_MODE_QT && p.n_ids != p.n_tgt + p.n_qry)
+        return fail(c, PFAAI_ERR_INVALID, "QT: n_ids must equal n_tgt + n_qry");
+    // T must hold every count < 2^16 (packed u16 LDS counters; c <= min T)
+    const int64_t tn = (int64_t)p.n_prot * p.t_cols;
+    for (int64_t i = 0; i < tn; ++i)
+        if (p.T[i] < 0 || p.T[i] > 65535) return fail(c, PFAAI_ERR_INVALID, "T entries must lie in [0, 65535]");
+
+    c->prob = p;
+    const int32_t ni = p.n_ids;
+    // output rows and derived maps
+    std::vector<int32_t> row_of(ni, -1), tcol_row(ni), tcol_col(ni);
+    c->row_genome_h.clear();
+    c->q_index_h.clear();
+    if (p.mode == PFAAI_MODE_ALL) {
+        for (int32_t g = 0; g < ni; ++g) { row_of[g] = g; c->row_genome_h.push_back(g); }
+        c->n_rows = ni;
+        c->n_pairs = (int64_t)ni * (ni - 1) / 2;
+        c->max_cols = ni - 1;
+        c->prob.n_qry = ni;
+        c->prob.n_tgt = 0;
+    } else if (p.mode == PFAAI_MODE_QSUB) {
+        c->row_genome_h.assign(p.n_qry, -1);
+        c->q_index_h.assign(p.q_index, p.q_index + ni);
+        for (int32_t g = 0; g < ni; ++g) {
+            if (!p.is_q[g]) continue;
+            const int32_t qi = p.q_index[g];
+            if (qi < 0 || qi >= p.n_qry) return fail(c, PFAAI_ERR_INVALID, "q_index out of range");
+            row_of[g] = qi;
+            c->row_genome_h[qi] = g;
+        }
+        for (int32_t x : c->row_genome_h)
+            if (x < 0) return fail(c, PFAAI_ERR_INVALID, "query list has holes");
+        c->n_rows = p.n_qry;
+        c->n_pairs = (int64_t)p.n_qry * p.n_tgt + (int64_t)p.n_qry * (p.n_qry - 1) / 2;
+        c->max_cols = ni;
+    } else {
+        for (int32_t q = 0; q < p.n_qry; ++q) {
+            row_of[p.n_tgt + q] = q;
+            c->row_genome_h.push_back(p.n_tgt + q);
+        }
+        c->n_rows = p.n_qry;
+        c->n_pairs = (int64_t)p.n_qry * p.n_tgt;
+        c->max_cols = p.n_tgt;
+    }
+    for (int32_t g = 0; g < ni; ++g) { tcol_row[g] = g; tcol_col[g] = g; }
+    // QT reference T-index quirk: the reference reads
+    // T[p][i / nT] and T[p][nQ + i % nT] for JAC index i = q*nT + t.  Both
+    // are per-genome remaps, applied only under PFAAI_FLAG_REF_COMPAT.
+    if (p.mode == PFAAI_MODE_QT) {
+        for (int32_t q = 0; q < p.n_qry; ++q) tcol_row[p.n_tgt + q] = q;
+        for (int32_t t = 0; t < p.n_tgt; ++t) tcol_col[t] = p.n_qry + t;
+        for (int32_t g = 0; g < ni; ++g)
+            if (tcol_row[g] >= p.t_cols || tcol_col[g] >= p.t_cols) {
+                // compat maps out of T: clamp to identity (compat is then undefined, as in the reference)
+                tcol_row[g] = std::min(tcol_row[g], p.t_cols - 1);
+                tcol_col[g] = std::min(tcol_col[g], p.t_cols - 1);
+            }
+    }
+    for (int32_t g = 0; g < ni; ++g)
+        if (g >= p.t_cols) return fail(c, PFAAI_ERR_INVALID, "T needs a column per genome id");
+
+    int rc;
+    if ((rc = upload(c, c->Lp, p.Lp, PFAAI_NTETRAMERS + 1))) return rc;
+    if ((rc = upload(c, c->Fp, p.F_prot, p.n_f))) return rc;
+    if ((rc = upload(c, c->Fg, p.F_genome, p.n_f))) return rc;
+    if ((rc = upload(c, c->T, p.T, tn))) return rc;
+    std::vector<uint8_t> isq(ni, 1);
+    if (p.is_q) isq.assign(p.is_q, p.is_q + ni);
+    if ((rc = upload(c, c->is_q, isq.data(), ni))) return rc;
+    std::vector<int32_t> qidx(ni, -1), trank(ni, -1);
+    if (p.q_index) qidx.assign(p.q_index, p.q_index + ni);
+    if (p.t_rank) trank.assign(p.t_rank, p.t_rank + ni);
+    if ((rc = upload(c, c->q_index, qidx.data(), ni))) return rc;
+    if ((rc = upload(c, c->t_rank, trank.data(), ni))) return rc;
+    if ((rc = upload(c, c->row_of, row_of.data(), ni))) return rc;
+    if ((rc = upload(c, c->row_genome, c->row_genome_h.data(), c->row_genome_h.size()))) return rc;
+    if ((rc = upload(c, c->tcol_row, tcol_row.data(), ni))) return rc;
+    if ((rc = upload(c, c->tcol_col, tcol_col.data(), ni))) return rc;
+
+    Dev& d = c->dev;
+    d.mode = p.mode;
+    d.n_ids = ni;
+    d.n_prot = p.n_prot;
+    d.t_cols = p.t_cols;
+    d.n_qry = c->prob.n_qry;
+    d.n_tgt = c->prob.n_tgt;
+    d.n_f = p.n_f;
+    d.Lp = static_cast<const int64_t*>(c->Lp.p);
+    d.Fp = static_cast<const int32_t*>(c->Fp.p);
+    d.Fg = static_cast<const int32_t*>(c->Fg.p);
+    d.T = static_cast<const int32_t*>(c->T.p);
+    d.is_q = static_cast<const uint8_t*>(c->is_q.p);
+    d.q_index = static_cast<const int32_t*>(c->q_index.p);
+    d.t_rank = static_cast<const int32_t*>(c->t_rank.p);
+    d.row_of = static_cast<const int32_t*>(c->row_of.p);
+    d.row_genome = static_cast<const int32_t*>(c->row_genome.p);
+    d.tcol_row = static_cast<const int32_t*>(c->tcol_row.p);
+    d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
+
+    // Work space sized for all rows, so pfaai_run never allocates or syncs:
+    // one counting pass over every row gives the exact record capacity.
+    const int64_t n = c->n_rows * p.n_prot;
+    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kScanTile));
+    if ((rc = ensure(c, c->cnt, n * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->rowptr, (n + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->cursor, (n + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->sums, tiles * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->recs, 8))) return rc;
+    HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
+    {
+        auto* cnt = static_cast<uint32_t*>(c->cnt.p);
+        auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+        HIPCHK(c, hipMemsetAsync(cnt, 0, n * sizeof(uint32_t), c->stream));
+        const int64_t rb = 0, re = c->n_rows;
+        switch (p.mode) {
+            case 0: hipLaunchKernelGGL((k_tetra_records<0, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
+            case 1: hipLaunchKernelGGL((k_tetra_records<1, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
+            default: hipLaunchKernelGGL((k_tetra_records<2, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
+        }
+        auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
+        auto* sums = static_cast<unsigned long long*>(c->sums.p);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kScanThreads), 0, c->stream, cnt, n, rowptr, sums);
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, c->stream, sums, tiles, sc + SC_GRAND);
+        hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, c->stream, rowptr, n, sums,
+                           sc + SC_GRAND, static_cast<unsigned long long*>(nullptr));
+        HIPCHK(c, hipGetLastError());
+        unsigned long long host_sc[SC_N];
+        HIPCHK(c, hipMemcpyAsync(host_sc, sc, sizeof(host_sc), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (host_sc[SC_ERR]) return fail(c, PFAAI_ERR_INVALID, "a tetramer block holds more than 4096 protein runs");
+        c->recs_cap = host_sc[SC_GRAND];
+        if ((rc = ensure(c, c->recs, std::max<uint64_t>(1, c->recs_cap) * sizeof(uint2)))) return rc;
+    }
+    c->loaded = true;
+    return PFAAI_OK;
+}
+
+int pfaai_shape(const pfaai_ctx* c, int64_t* n_rows, int64_t* n_pairs) {
+    if (!c || !c->loaded) return PFAAI_ERR_INVALID;
+    if (n_rows) *n_rows = c->n_rows;
+    if (n_pairs) *n_pairs = c->n_pairs;
+    return PFAAI_OK;
+}
+
+int pfaai_row_span(const pfaai_ctx* c, int64_t rb, int64_t re, int64_t* first, int64_t* count) {
+    if (!c || !c->loaded || rb < 0 || re > c->n_rows || rb > re) return PFAAI_ERR_INVALID;
+    const auto& p = c->prob;
+    int64_t f = 0, l = 0;  // [f, l)
+    if (rb == re) {
+        f = l = 0;
+    } else if (p.mode == PFAAI_MODE_ALL) {
+        const int64_t n = p.n_ids;
+        auto base = [n](int64_t a) { return n * a - a * (a + 1) / 2; };  // JAC index of (a, a+1)
+        f = base(rb);
+        l = base(re);
+    } else if (p.mode == PFAAI_MODE_QT) {
+        f = rb * p.n_tgt;
+        l = re * p.n_tgt;
+    } else {
+        f = rb * (int64_t)p.n_tgt;
+        l = c->n_pairs;  // triangle rows follow all cross rows: hull to the end
+        if (re == c->n_rows && rb == 0) f = 0;
+    }
+    if (first) *first = f;
+    if (count) *count = l - f;
+    return PFAAI_OK;
+}
+
+int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+              void* stream) {
+    if (!c) return PFAAI_ERR_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
+    if ((flags & PFAAI_FLAG_EMIT_JAC) && (!S || !N)) return fail(c, PFAAI_ERR_INVALID, "EMIT_JAC needs S and N");
+    if (!aji && !S && !N) return fail(c, PFAAI_ERR_INVALID, "no output");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
+        HIPCHK(c, hipStreamSynchronize(s));
+        c->pool_used = 0;
+    }
+    c->timed = true;
+    if (rb == re) return PFAAI_OK;
+    switch (c->prob.mode) {
+        case 0: return run_mode<0>(c, rb, re, flags, aji, S, N, s);
+        case 1: return run_mode<1>(c, rb, re, flags, aji, S, N, s);
+        default: return run_mode<2>(c, rb, re, flags, aji, S, N, s);
+    }
+}
+
+int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int32_t* h_N) {
+    if (!c) return PFAAI_ERR_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t np = c->n_pairs;
+    int rc;
+    if ((rc = ensure(c, c->out_aji, np * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_S, np * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_N, np * sizeof(int32_t)))) return rc;
+    auto* aji = static_cast<double*>(c->out_aji.p);
+    auto* S = static_cast<double*>(c->out_S.p);
+    auto* N = static_cast<int32_t*>(c->out_N.p);
+    HIPCHK(c, hipMemsetAsync(aji, 0, np * sizeof(double), c->stream));
+    HIPCHK(c, hipMemsetAsync(S, 0, np * sizeof(double), c->stream));
+    HIPCHK(c, hipMemsetAsync(N, 0, np * sizeof(int32_t), c->stream));
+    rc = pfaai_run(c, 0, c->n_rows, flags | PFAAI_FLAG_EMIT_JAC, aji, S, N, c->stream);
+    if (rc) return rc;
+    if (h_aji) HIPCHK(c, hipMemcpyAsync(h_aji, aji, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (h_S) HIPCHK(c, hipMemcpyAsync(h_S, S, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (h_N) HIPCHK(c, hipMemcpyAsync(h_N, N, np * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_OK;
+}
+
+int pfaai_last_stats(pfaai_ctx* c, int64_t* n_events, float* ms_build, float* ms_rows) {
+    if (!c) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned long long ev = 0;
+    HIPCHK(c, hipMemcpy(&ev, static_cast<unsigned long long*>(c->scalars.p) + SC_EVENTS, sizeof(ev),
+                        hipMemcpyDeviceToHost));
+    if (n_events) *n_events = (int64_t)ev;
+    if (c->timed) {
+        HIPCHK(c, hipEventSynchronize(c->ev2));
+        float a = 0.f, b = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&a, c->ev0, c->ev1));
+        HIPCHK(c, hipEventElapsedTime(&b, c->ev1, c->ev2));
+        if (ms_build) *ms_build = a;
+        if (ms_rows) *ms_rows = b;
+    }
+    return PFAAI_OK;
+}
+
+int pfaai_timing(pfaai_ctx* c, int reset, int32_t* n_runs, double* ms_build, double* ms_rows) {
+    if (!c) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    double b = 0.0, r = 0.0;
+    const size_t n = c->pool_used / 3;
+    for (size_t i = 0; i < n; ++i) {
+        hipEvent_t* ev = &c->pool[3 * i];
+        HIPCHK(c, hipEventSynchronize(ev[2]));
+        float x = 0.f, y = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&x, ev[0], ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&y, ev[1], ev[2]));
+        b += x;
+        r += y;
+    }
+    if (n_runs) *n_runs = (int32_t)n;
+    if (ms_build) *ms_build = b;
+    if (ms_rows) *ms_rows = r;
+    if (reset) {
+        c->pool_used = 0;
+        c->timed = false;
+    }
+    return PFAAI_OK;
+}
+
+int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
+    if (!c || !h_counts) return PFAAI_ERR_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    if (row < 0 || row >= c->n_rows) return fail(c, PFAAI_ERR_INVALID, "row out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    const auto& p = c->prob;
+    const int64_t cells = (int64_t)p.n_prot * p.n_ids;
+    int rc;
+    if ((rc = ensure(c, c->dbg, cells * sizeof(int32_t)))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->dbg.p, 0, cells * sizeof(int32_t), c->stream));
+    const int32_t chunk = 2 * 10 * kRowThreads;
+    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
+    const size_t lds = 10 * kRowThreads * sizeof(uint32_t);
+    auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
+    auto* recs = static_cast<const uint2*>(c->recs.p);
+    auto* out = static_cast<int32_t*>(c->dbg.p);
+    switch (p.mode) {
+        case 0:
+            if ((rc = build_records<0>(c, row, row + 1, c->stream, false))) return rc;
+            hipLaunchKernelGGL(k_row_counts<0>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
+            break;
+        case 1:
+            if ((rc = build_records<1>(c, row, row + 1, c->stream, false))) return rc;
+            hipLaunchKernelGGL(k_row_counts<1>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
+            break;
+        default:
+            if ((rc = build_records<2>(c, row, row + 1, c->stream, false))) return rc;
+            hipLaunchKernelGGL(k_row_counts<2>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
+            break;
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h_counts, out, cells * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_OK;
+}
+
+int pfaai_device_alloc(pfaai_ctx* c, void** ptr, int64_t bytes) {
+    if (!c || !ptr || bytes < 0) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(ptr, bytes > 0 ? bytes : 8));
+    return PFAAI_OK;
+}
+
+int pfaai_device_free(pfaai_ctx* c, void* ptr) {
+    if (!c) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (ptr) HIPCHK(c, hipFree(ptr));
+    return PFAAI_OK;
+}
+
+int pfaai_memcpy_d2h(pfaai_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c || bytes < 0) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return PFAAI_OK;
+}
+
+int pfaai_synchronize(pfaai_ctx* c) {
+    if (!c) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());
+    return PFAAI_OK;
+}
+
+}  // extern "C"

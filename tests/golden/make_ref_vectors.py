@@ -1,0 +1,81 @@
+"""Golden vectors produced by the reference itself on synthetic databases.
+
+Builds small SYN databases (parfastaai_amd/syn.py, deterministic), runs the
+reference CLI compiled from its own sources (oracle/_ref/par_fastaai.x, see
+oracle/build_ref.sh) on them and stores its output CSVs gzip'd under
+tests/golden/ref_<case>.csv.gz.  The tests regenerate the same arrays with
+syn.generate() and compare the HIP engine's matrix with these files.
+
+Run in the build container (needs oracle/_ref/par_fastaai.x):
+    python tests/golden/make_ref_vectors.py
+"""
+import gzip
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from parfastaai_amd import syn  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "par_fastaai.x")
+
+# name -> (kind, kwargs)
+CASES = {
+    # all-vs-all, 48 genomes x 24 SCPs, clades of 8
+    "all48": ("all", dict(n_genomes=48, n_prot=24, clade_size=8)),
+    # all-vs-all with sparse proteins (has=0.6) so some pairs miss proteins
+    "all32_sparse": ("all", dict(n_genomes=32, n_prot=16, clade_size=4, has=0.6, keep=0.7)),
+    # query subset (-q) with a sorted list of 7 genomes out of 40
+    "qsub40": ("qsub", dict(n_genomes=40, n_prot=20, clade_size=5, query=[1, 4, 9, 10, 22, 31, 39])),
+    # query-vs-target (-r), 12 targets x 12 queries (nQ == nT keeps the
+    # reference's column map intact; its T-index quirk is reproduced under
+    # ref-compat and pinned here)
+    "qt12": ("qt", dict(n_tgt=12, n_qry=12, n_prot=20, clade_size=4)),
+}
+
+
+def run_ref(args, out_csv):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run([REF, *args, out_csv], capture_output=True, text=True, env=env)
+    if r.returncode != 0:
+        raise RuntimeError(f"reference failed ({r.returncode}): {r.stderr[-2000:]}")
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("oracle/_ref/par_fastaai.x missing: run oracle/build_ref.sh")
+    with tempfile.TemporaryDirectory() as td:
+        for name, (kind, kw) in CASES.items():
+            out = os.path.join(td, name + ".csv")
+            if kind == "all":
+                db = os.path.join(td, name + ".db")
+                syn.write_db(db, **kw)
+                run_ref([db], out)
+            elif kind == "qsub":
+                kw = dict(kw)
+                query = kw.pop("query")
+                db = os.path.join(td, name + ".db")
+                g = syn.write_db(db, **kw)
+                ql = os.path.join(td, name + ".txt")
+                with open(ql, "w") as f:
+                    f.write("\n".join(g["genome_set"][i] for i in query) + "\n")
+                run_ref([db, "-q", ql], out)
+            else:
+                kw = dict(kw)
+                nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")
+                tdb, qdb = os.path.join(td, name + "_t.db"), os.path.join(td, name + "_q.db")
+                syn.write_db(tdb, n_genomes=nT, **kw)
+                syn.write_db(qdb, n_genomes=nQ, genome_prefix="qry", genome_seed=syn.DEFAULT_SEED + 1,
+                             n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
+                run_ref([tdb, "-r", qdb], out)
+            with open(out, "rb") as fi, gzip.GzipFile(os.path.join(HERE, f"ref_{name}.csv.gz"), "wb", mtime=0) as fo:
+                fo.write(fi.read())
+            print("wrote", name)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+"""Fixture loaders shared by the tests (reference golden vectors in tests/golden)."""
+import gzip
+import os
+
+import numpy as np
+
+from parfastaai_amd import formats as fm
+from parfastaai_amd.datastruct import ParFAAIData, ParFAAIQryTgtData, ParFAAIQSubData
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def gpath(name):
+    return os.path.join(GOLDEN, name + ".gz")
+
+
+def text(name):
+    return gzip.open(gpath(name)).read().decode()
+
+
+def xantho_names():
+    return fm.read_csv_matrix(gpath("xanthodb_aji_matrix_wheader.csv"))[1]
+
+
+def all_ds(prefix, names=None):
+    """ParFAAIData from a fixture prefix (xanthodb, xdb_subset1, xdb_subset2)."""
+    Lc = fm.read_vec_i32(gpath(prefix + "_lc_array.bin"))
+    F = fm.read_f_array(gpath(prefix + "_f_array.bin"))
+    T = fm.read_matrix_i32(gpath(prefix + "_t_matrix.bin"))
+    return ParFAAIData(Lc, F, T, names)
+
+
+def qsub_ds():
+    Lc = fm.read_vec_i32(gpath("xanthodb_lc_array.bin"))
+    F = fm.read_f_array(gpath("xanthodb_f_array.bin"))
+    T = fm.read_matrix_i32(gpath("xanthodb_t_matrix.bin"))
+    return ParFAAIQSubData(Lc, F, T, xantho_names(), text("qsub_test_input.txt").split())
+
+
+def qt_ds():
+    Lc = fm.read_vec_i32(gpath("xdb_qt_lc_array.bin"))
+    F = fm.read_f_array(gpath("xdb_qt_f_array.bin"))
+    T = fm.read_matrix_i32(gpath("xdb_qt_t_matrix.bin"))
+    return ParFAAIQryTgtData(Lc, F, T, [f"t{i}" for i in range(4)], [f"q{i}" for i in range(4)])
+
+
+ALL_FIXTURES = [("xanthodb", "xanthodb"), ("xdb_subset1", "xdb_subset1"), ("xdb_subset2", "xdb_subset2")]
+
+
+def jac_fixture(name):
+    return fm.read_jac(gpath(name + "_jac.bin")), fm.read_vec_f64(gpath(name + "_aji.bin"))
+
+
+def syn_case(name):
+    """(DataStruct, reference CSV matrix) for a tests/golden/ref_<name>.csv.gz case
+    (see tests/golden/make_ref_vectors.py)."""
+    import make_ref_vectors as mk  # noqa
+    from parfastaai_amd import syn
+    kind, kw = mk.CASES[name]
+    kw = dict(kw)
+    rows, cols, M = fm.read_csv_matrix(gpath(f"ref_{name}.csv"))
+    if kind == "all":
+        g = syn.generate(**kw)
+        ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"])
+    elif kind == "qsub":
+        query = kw.pop("query")
+        g = syn.generate(**kw)
+        ds = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"],
+                                        [g["genome_set"][i] for i in query])
+    else:
+        ds = qt_syn(kw)
+    return ds, M
+
+
+def qt_syn(kw):
+    """QT arrays for two SYN DBs exactly as the reference's QT loader joins
+    them (scp_db.hpp:450-528): per (t, p) block target genomes then query
+    genomes offset by nT, only tetramers present in both; T side by side."""
+    from parfastaai_amd import syn
+    kw = dict(kw)
+    nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")
+    gt = syn.generate(n_genomes=nT, **kw)
+    gq = syn.generate(n_genomes=nQ, genome_seed=syn.DEFAULT_SEED + 1,
+                      n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
+    P = gt["T"].shape[0]
+    blocks_t = _blocks(gt)
+    blocks_q = _blocks(gq)
+    t_l, p_l, g_l = [], [], []
+    for key in sorted(set(blocks_t) & set(blocks_q)):
+        t, p = key
+        g = np.concatenate([blocks_t[key], blocks_q[key] + nT])
+        t_l.append(np.full(len(g), t)); p_l.append(np.full(len(g), p)); g_l.append(g)
+    t = np.concatenate(t_l); p = np.concatenate(p_l); g = np.concatenate(g_l)
+    Lc = np.bincount(t, minlength=160000)
+    T = np.concatenate([gt["T"], gq["T"]], axis=1)
+    F = np.stack([p, g], axis=1).astype(np.int32)
+    return ParFAAIQryTgtData(Lc, F, T, gt["genome_set"], syn.genome_names(nQ, "qry"), gt["protein_set"][:P])
+
+
+def _blocks(g):
+    out = {}
+    Lp, Fp, Fg = g["Lp"], g["F_prot"], g["F_genome"]
+    nz = np.nonzero(np.diff(Lp))[0]
+    for t in nz:
+        s, e = Lp[t], Lp[t + 1]
+        ps = Fp[s:e]
+        cut = np.flatnonzero(np.r_[True, ps[1:] != ps[:-1], True])
+        for a, b in zip(cut[:-1], cut[1:]):
+            out[(int(t), int(ps[a]))] = Fg[s + a:s + b].astype(np.int64)
+    return out

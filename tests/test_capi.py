@@ -1,0 +1,57 @@
+"""The C-ABI library builds, loads and exports every symbol include/pfaai_hip.h
+declares (CPU only: no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from parfastaai_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "pfaai_hip.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(pfaai_\w+)\s*\(", src, re.M)))
+
+
+def test_header_lists_exports():
+    assert header_functions() == sorted(_capi.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    lib = _capi.load_library()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+        assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
+
+
+def test_abi_version():
+    assert _capi.load_library().pfaai_version() == 1
+
+
+def test_problem_struct_layout():
+    # pfaai_problem: 6 x int32, int64, 7 pointers
+    assert ctypes.sizeof(_capi.Problem) == 6 * 4 + 8 + 7 * 8
+
+
+def test_no_silent_cpu_fallback_without_gpu():
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present")
+    with pytest.raises(_capi.PfaaiError):
+        _capi.Engine(0)
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "parfastaai_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                txt = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert "import oracle" not in txt and "pfaai_oracle" not in txt, f

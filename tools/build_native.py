@@ -1,0 +1,99 @@
+"""Build recipes for the native pieces (no cmake, no pip).
+
+  hip      parfastaai_amd/lib/libpfaai_hip.so   hipcc --offload-arch=gfx950
+  cli      parfastaai_amd/lib/par_fastaai_amd   g++ host CLI over the C ABI
+  syn      tools/_build/libpfaai_syn.so         synthetic DB generator
+  oracle   oracle/_build/libpfaai_oracle.so     CPU oracle (test infra)
+  ref      oracle/_ref/par_fastaai.x            the reference, from its own
+                                                sources (only where
+                                                /root/reference exists)
+Everything is built in-tree so the snapshot that travels to the GPU box
+carries the binaries.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PFAAI_ARCH", "gfx950")
+
+
+def _run(cmd, cwd=ROOT):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, cwd=cwd, check=True)
+
+
+def _newer(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build_hip(force=False):
+    src = os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_hip.hip")
+    deps = [src, os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_kernels.hpp"), os.path.join(ROOT, "include/pfaai_hip.h")]
+    out = os.path.join(ROOT, "parfastaai_amd/lib/libpfaai_hip.so")
+    if force or _newer(out, deps):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
+              "-ffp-contract=off", "-fno-fast-math", "-Wall", "-I" + os.path.join(ROOT, "include"),
+              "-o", out, src])
+    return out
+
+
+def build_syn(force=False):
+    src = os.path.join(ROOT, "tools/syn_gen.c")
+    out = os.path.join(ROOT, "tools/_build/libpfaai_syn.so")
+    if force or _newer(out, [src]):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-std=c11", "-o", out, src])
+    return out
+
+
+def build_oracle(force=False):
+    src = os.path.join(ROOT, "oracle/pfaai_oracle.c")
+    out = os.path.join(ROOT, "oracle/_build/libpfaai_oracle.so")
+    if force or _newer(out, [src]):
+        _run(["make", "-C", os.path.join(ROOT, "oracle")])
+    return out
+
+
+def build_cli(force=False):
+    srcs = [os.path.join(ROOT, "parfastaai_amd/host", f) for f in ("par_fastaai_amd.cpp",)]
+    hdrs = [os.path.join(ROOT, "parfastaai_amd/host", f) for f in os.listdir(os.path.join(ROOT, "parfastaai_amd/host"))]
+    if not os.path.exists(srcs[0]):
+        return None
+    out = os.path.join(ROOT, "parfastaai_amd/lib/par_fastaai_amd")
+    if force or _newer(out, srcs + hdrs + [os.path.join(ROOT, "include/pfaai_hip.h")]):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-fopenmp", "-I" + os.path.join(ROOT, "include"), "-o", out,
+              *srcs, "-L" + os.path.join(ROOT, "parfastaai_amd/lib"), "-lpfaai_hip",
+              "-Wl,-rpath,$ORIGIN", "/lib/x86_64-linux-gnu/libsqlite3.so.0", "-ldl"])
+    return out
+
+
+def build_ref(force=False):
+    """The reference CLI compiled from its own sources under /root/reference
+    (oracle/build_ref.sh); skipped where the reference is absent."""
+    if not os.path.isdir("/root/reference/src"):
+        return None
+    out = os.path.join(ROOT, "oracle/_ref/par_fastaai.x")
+    if force or not os.path.exists(out):
+        _run(["bash", os.path.join(ROOT, "oracle/build_ref.sh")])
+    return out
+
+
+def build_all(force=False):
+    outs = [build_hip(force), build_syn(force), build_oracle(force), build_cli(force)]
+    try:
+        outs.append(build_ref(force))
+    except subprocess.CalledProcessError as e:  # the reference build is optional
+        print(f"reference build failed: {e}", file=sys.stderr)
+    return outs
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
