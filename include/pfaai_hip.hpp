@@ -1,0 +1,162 @@
+// pfaai_hip.hpp -- C++ adapter with the reference's ParFAAIImpl surface over
+// the C ABI of libpfaai_hip.so.
+//
+// Drop-in for  ParFAAIImpl<IdType, ValueType, DSIT>
+//              (reference include/pfaai/algorithm_impl.hpp:38-357):
+//   explicit ParFAAIHipImpl(const DSIT&);  int run();  int computeJAC();
+//   int computeAJI();  const std::vector<JACType>& getJAC() const;
+//   const std::vector<ValueType>& getAJI() const;
+// DSIT is any type with the reference's DataStructInterface accessors
+// (interface.hpp:200-328): refLp(), refLc(), refF() (elements with .first/
+// .second), refT() (operator()(p, g), rows(), cols()), initJAC(),
+// nGenomePairs(), qrySetSize(), tgtSetSize(), isQryGenome(), mapQueryId(),
+// plus the JACType typedef -- the reference's own ParFAAIData /
+// ParFAAIQSubData / ParFAAIQryTgtData qualify unchanged, and so do the host
+// classes of parfastaai_amd/host/datastruct.hpp.  The mode is deduced from the
+// DSIT (pfaai_mode_of<DSIT>) or passed explicitly.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pfaai_hip.h"
+
+namespace pfaai {
+
+struct HipError : std::runtime_error {
+    int code;
+    HipError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+template <typename IdType, typename ValueType, typename DSIT>
+class ParFAAIHipImpl {
+  public:
+    using JACType = typename DSIT::JACType;
+
+    // mode: PFAAI_MODE_ALL / QSUB / QT (the three reference DSIT classes)
+    explicit ParFAAIHipImpl(const DSIT& ds, int mode, int device = 0, bool ref_compat = false)
+        : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
+        int rc = pfaai_create(&m_ctx, device);
+        if (rc) throw HipError(rc, "pfaai_create failed (no visible MI355X?)");
+        upload();
+    }
+    ~ParFAAIHipImpl() { pfaai_destroy(m_ctx); }
+    ParFAAIHipImpl(const ParFAAIHipImpl&) = delete;
+    ParFAAIHipImpl& operator=(const ParFAAIHipImpl&) = delete;
+
+    // algorithm_impl.hpp:281-306
+    int computeJAC() {
+        m_JAC = m_ds.initJAC();
+        if (m_mode == PFAAI_MODE_QT && !m_compat) {
+            // correct QT ids = the E ids (query nT + q, target t); SURVEY 8a row Q
+            const int64_t nT = m_ds.tgtSetSize();
+            for (std::size_t i = 0; i < m_JAC.size(); ++i) {
+                m_JAC[i].genomeA = static_cast<IdType>(nT + (int64_t)i / nT);
+                m_JAC[i].genomeB = static_cast<IdType>((int64_t)i % nT);
+            }
+        }
+        const std::size_t n = m_JAC.size();
+        std::vector<double> S(n);
+        std::vector<int32_t> N(n);
+        m_AJIdev.resize(n);
+        int rc = pfaai_compute(m_ctx, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, m_AJIdev.data(), S.data(), N.data());
+        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        for (std::size_t i = 0; i < n; ++i) {
+            m_JAC[i].S = S[i];
+            m_JAC[i].N = N[i];
+        }
+        pfaai_last_stats(m_ctx, &m_events, &m_msBuild, &m_msRows);
+        return 0;  // PFAAI_OK
+    }
+    // algorithm_impl.hpp:309-322 (the kernel epilogue already divided S / N)
+    int computeAJI() {
+        if (m_AJIdev.size() != m_JAC.size() || m_JAC.empty()) computeJAC();
+        m_AJI.assign(m_AJIdev.begin(), m_AJIdev.end());
+        return 0;
+    }
+    // algorithm_impl.hpp:325-329
+    int run() {
+        computeJAC();
+        computeAJI();
+        return 0;
+    }
+    const std::vector<JACType>& getJAC() const { return m_JAC; }
+    const std::vector<ValueType>& getAJI() const { return m_AJI; }
+    int64_t nEvents() const { return m_events; }
+    float msBuild() const { return m_msBuild; }
+    float msRows() const { return m_msRows; }
+
+  private:
+    void upload() {
+        const auto& Lp32 = m_ds.refLp();
+        const auto& Lc = m_ds.refLc();
+        const auto& F = m_ds.refF();
+        const auto& T = m_ds.refT();
+        const int64_t nf = (int64_t)F.size();
+        m_Lp.assign(PFAAI_NTETRAMERS + 1, 0);
+        for (int t = 0; t < PFAAI_NTETRAMERS; ++t) m_Lp[t + 1] = m_Lp[t] + (int64_t)Lc[t];
+        (void)Lp32;
+        m_Fp.resize(nf);
+        m_Fg.resize(nf);
+        for (int64_t i = 0; i < nf; ++i) {
+            m_Fp[i] = F[i].first;
+            m_Fg[i] = F[i].second;
+        }
+        const int64_t P = (int64_t)T.rows(), C = (int64_t)T.cols();
+        m_T.resize(P * C);
+        for (int64_t p = 0; p < P; ++p)
+            for (int64_t g = 0; g < C; ++g) m_T[p * C + g] = T(p, g);
+        pfaai_problem pb{};
+        pb.mode = m_mode;
+        pb.n_prot = (int32_t)P;
+        pb.t_cols = (int32_t)C;
+        pb.n_f = nf;
+        pb.Lp = m_Lp.data();
+        pb.F_prot = m_Fp.data();
+        pb.F_genome = m_Fg.data();
+        pb.T = m_T.data();
+        if (m_mode == PFAAI_MODE_ALL) {
+            pb.n_ids = (int32_t)m_ds.tgtSetSize();
+        } else if (m_mode == PFAAI_MODE_QSUB) {
+            const int32_t n = (int32_t)m_ds.tgtSetSize();
+            pb.n_ids = n;
+            pb.n_qry = (int32_t)m_ds.qrySetSize();
+            pb.n_tgt = n - pb.n_qry;
+            m_isq.resize(n);
+            m_qidx.assign(n, -1);
+            m_trank.assign(n, -1);
+            for (int32_t g = 0; g < n; ++g) {  // mapQueryId = genome index map (ds_impl.hpp:264)
+                m_isq[g] = m_ds.isQryGenome(g) ? 1 : 0;
+                (m_isq[g] ? m_qidx[g] : m_trank[g]) = (int32_t)m_ds.mapQueryId(g);
+            }
+            pb.is_q = m_isq.data();
+            pb.q_index = m_qidx.data();
+            pb.t_rank = m_trank.data();
+        } else {
+            pb.n_tgt = (int32_t)m_ds.tgtSetSize();
+            pb.n_qry = (int32_t)m_ds.qrySetSize();
+            pb.n_ids = pb.n_tgt + pb.n_qry;
+            m_isq.assign(pb.n_ids, 0);
+            for (int32_t g = pb.n_tgt; g < pb.n_ids; ++g) m_isq[g] = 1;
+            pb.is_q = m_isq.data();
+        }
+        int rc = pfaai_load(m_ctx, &pb);
+        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+    }
+
+    const DSIT& m_ds;
+    int m_mode;
+    bool m_compat;
+    pfaai_ctx* m_ctx = nullptr;
+    std::vector<int64_t> m_Lp;
+    std::vector<int32_t> m_Fp, m_Fg, m_T, m_qidx, m_trank;
+    std::vector<uint8_t> m_isq;
+    std::vector<JACType> m_JAC;
+    std::vector<double> m_AJIdev;
+    std::vector<ValueType> m_AJI;
+    int64_t m_events = 0;
+    float m_msBuild = 0.f, m_msRows = 0.f;
+};
+
+}  // namespace pfaai

@@ -367,7 +367,7 @@ __global__ __launch_bounds__(kRowThreads) void k_rows(
     uint32_t N[KW];
 #pragma unroll
     for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
-    const int32_t tca = d.tcol_row[a];
+    const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
     uint32_t ev = 0;
     __syncthreads();
 

@@ -1,0 +1,261 @@
+// scp_db.hpp -- SQLite SCP/tetramer loader for the host CLI.
+//
+// Same SQL, same id rules and the same resulting arrays as the reference's
+// DB layer:
+//   SQLiteHelper        include/pfaai/db_helper.hpp:33-219
+//   SQLiteSCPDataBase   include/pfaai/scp_db.hpp:59-263
+//   QTSQLiteSCPDataBase include/pfaai/scp_db.hpp:267-590
+// Instead of one giant UNION ALL ... ORDER BY per thread (scp_db.hpp:161-216)
+// every protein's `<p>_tetras` table is read by its own read-only connection
+// in parallel (OpenMP) and F is assembled by a stable counting sort on the
+// tetramer id -- the same (tetramer, protein, blob order) layout.
+#pragma once
+#include <omp.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sqlite_min.h"
+
+namespace pfaai_host {
+
+constexpr int kNTetramers = 160000;
+
+struct DPair {
+    int32_t first, second;
+};
+
+struct DMatrix {
+    std::size_t nrows = 0, ncols = 0;
+    std::vector<int32_t> data;
+    DMatrix() = default;
+    DMatrix(std::size_t r, std::size_t c) : nrows(r), ncols(c), data(r * c, 0) {}
+    int32_t& operator()(std::size_t i, std::size_t j) { return data[i * ncols + j]; }
+    int32_t operator()(std::size_t i, std::size_t j) const { return data[i * ncols + j]; }
+    std::size_t rows() const { return nrows; }
+    std::size_t cols() const { return ncols; }
+};
+
+struct DBMetaData {
+    std::vector<std::string> proteinSet, genomeSet, qyGenomeSet;
+};
+
+struct LoadedArrays {
+    std::vector<int32_t> Lc;
+    std::vector<DPair> F;
+    DMatrix T;
+};
+
+class Conn {
+  public:
+    explicit Conn(const std::string& path) {
+        rc = sqlite3_open_v2(path.c_str(), &db, SQLITE_OPEN_READONLY, nullptr);
+    }
+    ~Conn() {
+        if (db) sqlite3_close(db);
+    }
+    Conn(const Conn&) = delete;
+    Conn& operator=(const Conn&) = delete;
+    bool ok() const { return rc == SQLITE_OK && db; }
+    std::string error() const { return db ? sqlite3_errmsg(db) : sqlite3_errstr(rc); }
+    int exec(const std::string& sql) { return sqlite3_exec(db, sql.c_str(), nullptr, nullptr, nullptr); }
+
+    // run a query, call fn(stmt) per row; returns SQLITE_OK or the error code
+    template <typename Fn>
+    int each(const std::string& sql, Fn&& fn) {
+        sqlite3_stmt* st = nullptr;
+        int e = sqlite3_prepare_v2(db, sql.c_str(), -1, &st, nullptr);
+        if (e != SQLITE_OK) {
+            last_sql = sql;
+            return e;
+        }
+        while ((e = sqlite3_step(st)) == SQLITE_ROW) fn(st);
+        sqlite3_finalize(st);
+        return e == SQLITE_DONE ? SQLITE_OK : e;
+    }
+
+    sqlite3* db = nullptr;
+    int rc = 0;
+    std::string last_sql;
+};
+
+inline std::vector<std::string> column_strings(Conn& c, const std::string& sql, int* err) {
+    std::vector<std::string> out;
+    *err = c.each(sql, [&](sqlite3_stmt* st) {
+        const unsigned char* s = sqlite3_column_text(st, 0);
+        out.emplace_back(s ? reinterpret_cast<const char*>(s) : "");
+    });
+    return out;
+}
+
+// per-protein (tetramer, genome list) rows, in table order
+struct ProteinRows {
+    std::vector<int32_t> tet, cnt, genomes;
+    int err = SQLITE_OK;
+};
+
+// Assemble Lc and F (tetramer, protein, blob order) from per-protein rows.
+inline void assemble_f(const std::vector<ProteinRows>& rows, LoadedArrays& out) {
+    out.Lc.assign(kNTetramers, 0);
+    for (const auto& r : rows)
+        for (std::size_t k = 0; k < r.tet.size(); ++k) out.Lc[r.tet[k]] += r.cnt[k];
+    std::vector<int64_t> cur(kNTetramers + 1, 0);
+    for (int t = 0; t < kNTetramers; ++t) cur[t + 1] = cur[t] + out.Lc[t];
+    out.F.resize(cur[kNTetramers]);
+    // protein-major pass: within a tetramer, proteins arrive in index order
+    for (std::size_t p = 0; p < rows.size(); ++p) {
+        const auto& r = rows[p];
+        std::size_t off = 0;
+        for (std::size_t k = 0; k < r.tet.size(); ++k) {
+            int64_t& pos = cur[r.tet[k]];
+            for (int32_t j = 0; j < r.cnt[k]; ++j) out.F[pos++] = DPair{(int32_t)p, r.genomes[off + j]};
+            off += r.cnt[k];
+        }
+    }
+}
+
+// SQLiteSCPDataBase: one DB, genome ids = genome_metadata order.
+inline int load_single(const std::string& path, DBMetaData& meta, LoadedArrays& out, std::string& err) {
+    Conn c(path);
+    if (!c.ok()) {
+        err = "Error in opening " + path + ": " + c.error();
+        return 1;  // PFAAI_ERR_SQLITE_DB
+    }
+    int e = 0;
+    meta.proteinSet = column_strings(c, "SELECT DISTINCT scp_acc FROM scp_data", &e);  // db_helper.hpp:195-215
+    if (e == SQLITE_OK) meta.genomeSet = column_strings(c, "SELECT genome_name FROM genome_metadata", &e);
+    if (e != SQLITE_OK) {
+        err = "Error in reading metadata of " + path + ": " + c.error();
+        return 1;
+    }
+    const int P = (int)meta.proteinSet.size();
+    const int G = (int)meta.genomeSet.size();
+    std::vector<ProteinRows> rows(P);
+    out.T = DMatrix(P, G);
+    int bad = 0;
+#pragma omp parallel
+    {
+        Conn tc(path);  // one read-only connection per thread
+#pragma omp for schedule(dynamic, 1)
+        for (int p = 0; p < P; ++p) {
+            if (!tc.ok()) {
+                rows[p].err = 1;
+                continue;
+            }
+            auto& r = rows[p];
+            const std::string& acc = meta.proteinSet[p];
+            r.err = tc.each("SELECT tetramer, genomes FROM `" + acc + "_tetras`", [&](sqlite3_stmt* st) {
+                const int32_t t = sqlite3_column_int(st, 0);
+                const int nb = sqlite3_column_bytes(st, 1) / 4;
+                const auto* g = static_cast<const int32_t*>(sqlite3_column_blob(st, 1));
+                r.tet.push_back(t);
+                r.cnt.push_back(nb);
+                r.genomes.insert(r.genomes.end(), g, g + nb);
+            });
+            if (r.err == SQLITE_OK)  // proteinTetramerCounts (scp_db.hpp:219-262)
+                r.err = tc.each("SELECT genome_id, length(tetramers) FROM `" + acc + "_genomes`",
+                                [&](sqlite3_stmt* st) {
+                                    const int gid = sqlite3_column_int(st, 0);
+                                    if (gid >= 0 && gid < G) out.T(p, gid) = sqlite3_column_int(st, 1) / 4;
+                                });
+            for (int32_t t : r.tet)
+                if (t < 0 || t >= kNTetramers) r.err = 1;
+            for (int32_t g : r.genomes)
+                if (g < 0 || g >= G) r.err = 1;
+        }
+    }
+    for (int p = 0; p < P; ++p)
+        if (rows[p].err) {
+            err = "Error in reading tables of protein " + meta.proteinSet[p] + " from " + path;
+            bad = 1;
+            break;
+        }
+    if (bad) return 3;  // PFAAI_ERR_CONSTRUCT
+    assemble_f(rows, out);
+    return 0;
+}
+
+// QTSQLiteSCPDataBase: target DB `main` + ATTACHed query DB `QueryDB`;
+// shared proteins only, tetramers present in both (inner join), query
+// genome ids offset by the number of target genomes.
+inline int load_qt(const std::string& tgt, const std::string& qry, DBMetaData& meta, LoadedArrays& out,
+                   std::string& err) {
+    Conn c(tgt);
+    if (!c.ok()) {
+        err = "Error in opening " + tgt + ": " + c.error();
+        return 1;
+    }
+    if (c.exec("ATTACH DATABASE '" + qry + "' as QueryDB ;") != SQLITE_OK) {
+        err = "Error in attaching query database : " + qry + ": " + c.error();
+        return 1;
+    }
+    int e = 0;
+    meta.proteinSet = column_strings(c,
+                                     "SELECT DISTINCT target_table.scp_acc \n"
+                                     "  FROM `main`.scp_data as target_table, `QueryDB`.scp_data as query_table \n"
+                                     "  WHERE target_table.scp_acc = query_table.scp_acc;",
+                                     &e);  // db_helper.hpp:109-166
+    if (e == SQLITE_OK) meta.genomeSet = column_strings(c, "SELECT genome_name FROM `main`.genome_metadata", &e);
+    if (e == SQLITE_OK) meta.qyGenomeSet = column_strings(c, "SELECT genome_name FROM `QueryDB`.genome_metadata", &e);
+    if (e != SQLITE_OK) {
+        err = "Error in reading metadata: " + c.error();
+        return 1;
+    }
+    const int P = (int)meta.proteinSet.size();
+    const int nT = (int)meta.genomeSet.size(), nQ = (int)meta.qyGenomeSet.size();
+    std::vector<ProteinRows> rows(P);
+    out.T = DMatrix(P, nT + nQ);
+#pragma omp parallel
+    {
+        Conn tc(tgt);
+        bool ok = tc.ok() && tc.exec("ATTACH DATABASE '" + qry + "' as QueryDB ;") == SQLITE_OK;
+#pragma omp for schedule(dynamic, 1)
+        for (int p = 0; p < P; ++p) {
+            auto& r = rows[p];
+            if (!ok) {
+                r.err = 1;
+                continue;
+            }
+            const std::string& acc = meta.proteinSet[p];
+            r.err = tc.each("SELECT target_table.tetramer, target_table.genomes, query_table.genomes "
+                            "FROM main.`" + acc + "_tetras` as target_table, QueryDB.`" + acc +
+                                "_tetras` as query_table WHERE target_table.tetramer = query_table.tetramer",
+                            [&](sqlite3_stmt* st) {
+                                const int32_t t = sqlite3_column_int(st, 0);
+                                const int nt = sqlite3_column_bytes(st, 1) / 4, nq = sqlite3_column_bytes(st, 2) / 4;
+                                const auto* gt = static_cast<const int32_t*>(sqlite3_column_blob(st, 1));
+                                const auto* gq = static_cast<const int32_t*>(sqlite3_column_blob(st, 2));
+                                r.tet.push_back(t);
+                                r.cnt.push_back(nt + nq);
+                                r.genomes.insert(r.genomes.end(), gt, gt + nt);
+                                for (int j = 0; j < nq; ++j) r.genomes.push_back(nT + gq[j]);
+                            });
+            if (r.err == SQLITE_OK)
+                r.err = tc.each("SELECT genome_id, length(tetramers) FROM main.`" + acc + "_genomes`",
+                                [&](sqlite3_stmt* st) {
+                                    const int gid = sqlite3_column_int(st, 0);
+                                    if (gid >= 0 && gid < nT) out.T(p, gid) += sqlite3_column_int(st, 1) / 4;
+                                });
+            if (r.err == SQLITE_OK)
+                r.err = tc.each("SELECT genome_id, length(tetramers) FROM QueryDB.`" + acc + "_genomes`",
+                                [&](sqlite3_stmt* st) {
+                                    const int gid = sqlite3_column_int(st, 0);
+                                    if (gid >= 0 && gid < nQ) out.T(p, nT + gid) += sqlite3_column_int(st, 1) / 4;
+                                });
+            for (int32_t g : r.genomes)
+                if (g < 0 || g >= nT + nQ) r.err = 1;
+        }
+    }
+    for (int p = 0; p < P; ++p)
+        if (rows[p].err) {
+            err = "Error in reading tables of protein " + meta.proteinSet[p];
+            return 3;
+        }
+    assemble_f(rows, out);
+    return 0;
+}
+
+}  // namespace pfaai_host
