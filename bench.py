@@ -139,6 +139,8 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=320)
+    ap.add_argument("--f-only", action="store_true",
+                    help="give the engine F only (device radix-sort transposition instead of G)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -159,6 +161,8 @@ def main():
     n_f = len(g["F_genome"])
     log(f"generated SYN N={args.genomes} P={args.prot} |F|={n_f} in {time.perf_counter() - t0:.1f}s")
     ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    if not args.f_only:  # the DB's genome-major <p>_genomes lists: sort-free work lists
+        ds.with_genome_major(g["G_off"], g["G_tet"])
     eng = _capi.Engine(local)
     t0 = time.perf_counter()
     eng.load(**ds.problem())

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PFAAI_ABI_VERSION 1
+#define PFAAI_ABI_VERSION 2
 #define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
 
 /* Error codes: 0..3 mirror PFAAI_ERROR_CODE (interface.hpp:39-44). */
@@ -76,6 +76,15 @@ typedef struct {
     const uint8_t* is_q;   /* [n_ids] QSUB/QT: 1 for query genomes (NULL for ALL) */
     const int32_t* q_index; /* [n_ids] QSUB: position of the genome in the query file, -1 otherwise */
     const int32_t* t_rank; /* [n_ids] QSUB: rank among the non-query genomes, -1 otherwise */
+    /* Optional genome-major view (NULL if absent): the `<p>_genomes` blobs of
+     * the SCP database (scp_db.hpp:219-262 reads only their lengths), as a
+     * (genome, protein)-major CSR: tetramers of genome g, protein p are
+     * G_tet[G_off[g*n_prot+p] .. G_off[g*n_prot+p+1]).  With it the work
+     * lists are built without a sort (one run table + one binary search per
+     * entry); without it F is transposed on the device by a radix sort.
+     * Entries whose tetramer block is absent from F are ignored. */
+    const int64_t* G_off;  /* [n_ids * n_prot + 1] */
+    const int32_t* G_tet;  /* [G_off[n_ids * n_prot]] */
 } pfaai_problem;
 
 /* ---- lifecycle ---------------------------------------------------------- */

@@ -48,7 +48,7 @@ class Problem(ctypes.Structure):
         ("n_f", ctypes.c_int64),
         ("Lp", ctypes.c_void_p), ("F_prot", ctypes.c_void_p), ("F_genome", ctypes.c_void_p),
         ("T", ctypes.c_void_p), ("is_q", ctypes.c_void_p), ("q_index", ctypes.c_void_p),
-        ("t_rank", ctypes.c_void_p),
+        ("t_rank", ctypes.c_void_p), ("G_off", ctypes.c_void_p), ("G_tet", ctypes.c_void_p),
     ]
 
 
@@ -124,7 +124,7 @@ class Engine:
 
     # -- problem ----------------------------------------------------------------
     def load(self, *, mode, n_ids, n_prot, Lp, F_prot, F_genome, T, n_qry=0, n_tgt=0,
-             is_q=None, q_index=None, t_rank=None):
+             is_q=None, q_index=None, t_rank=None, G_off=None, G_tet=None):
         Lp = np.ascontiguousarray(Lp, dtype=np.int64)
         F_prot = np.ascontiguousarray(F_prot, dtype=np.int32)
         F_genome = np.ascontiguousarray(F_genome, dtype=np.int32)
@@ -132,12 +132,14 @@ class Engine:
         is_q = None if is_q is None else np.ascontiguousarray(is_q, dtype=np.uint8)
         q_index = None if q_index is None else np.ascontiguousarray(q_index, dtype=np.int32)
         t_rank = None if t_rank is None else np.ascontiguousarray(t_rank, dtype=np.int32)
+        G_off = None if G_off is None else np.ascontiguousarray(G_off, dtype=np.int64)
+        G_tet = None if G_tet is None else np.ascontiguousarray(G_tet, dtype=np.int32)
         assert Lp.shape == (NTETRAMERS + 1,)
         assert T.ndim == 2 and T.shape[0] == n_prot
         pb = Problem(mode=mode, n_ids=n_ids, n_prot=n_prot, t_cols=T.shape[1], n_qry=n_qry,
                      n_tgt=n_tgt, n_f=F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
                      F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
-                     t_rank=_ptr(t_rank))
+                     t_rank=_ptr(t_rank), G_off=_ptr(G_off), G_tet=_ptr(G_tet))
         self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
 
     def shape(self):

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -39,15 +40,18 @@ struct pfaai_ctx {
     int32_t max_cols = 0;
 
     // device-resident problem
-    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col;
+    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
+    bool has_g = false;
     Dev dev{};
 
-    // work space
-    DevBuf cnt, rowptr, cursor, recs, sums, scalars, out_aji, out_S, out_N, dbg;
-    uint64_t recs_cap = 0;  // records needed by the whole problem (all rows)
+    // work space (sized at load for all rows, so runs never allocate)
+    DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
+    DevBuf out_aji, out_S, out_N, dbg;
+    std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool timed = false;
+    int occupancy = 2;  // k_rows variant: workgroups per CU (PFAAI_ROWS_OCC=1|2)
     // per-run event triples for pfaai_timing (pool reused after each reset)
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;
@@ -56,7 +60,7 @@ struct pfaai_ctx {
 namespace {
 
 // scalars buffer layout (u64 each)
-enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_N = 4 };
+enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
 
 int fail(pfaai_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -105,33 +109,107 @@ int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Work-list build for rows [rb, re): counts, exclusive scan, fill.
+// exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
+int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
+
+// Work-list build for rows [rb, re): entries, LSD radix sort, rowptr.
 template <int MODE>
 int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool first_event) {
-    const int64_t n = (re - rb) * c->prob.n_prot;
-    auto* cnt = static_cast<uint32_t*>(c->cnt.p);
-    auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
-    auto* cursor = static_cast<unsigned long long*>(c->cursor.p);
-    auto* sums = static_cast<unsigned long long*>(c->sums.p);
+    const int64_t P = c->prob.n_prot;
+    const int64_t K = (re - rb) * P;  // keys
+    const int64_t n = c->row_fprefix[re] - c->row_fprefix[rb];  // entries (exact, from F at load)
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
-    HIPCHK(c, hipMemsetAsync(cnt, 0, n * sizeof(uint32_t), s));
-    const int grid = kNTetramers;  // one workgroup per tetramer block
-    hipLaunchKernelGGL((k_tetra_records<MODE, 0>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
-                       cnt, nullptr, nullptr, nullptr, err);
-    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kScanTile));
-    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kScanThreads), 0, s, cnt, n, rowptr, sums);
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, s, sums, tiles, sc + SC_GRAND);
-    hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, s, rowptr, n, sums, sc + SC_GRAND,
-                       cursor);
-    hipLaunchKernelGGL((k_tetra_records<MODE, 1>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
-                       nullptr, cursor, static_cast<uint2*>(c->recs.p), nullptr, err);
-    if (first_event) {
-        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL((k_tetra_records<MODE, 2>), dim3(grid), dim3(kTetraThreads), 0, s, c->dev, rb, re,
-                           nullptr, nullptr, nullptr, sc + SC_FIRST_KEY, err);
+    auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
+    auto* key_c = static_cast<uint32_t*>(c->key_c.p);
+    auto* rec_c = static_cast<uint2*>(c->rec_c.p);
+    HIPCHK(c, hipMemsetAsync(sc + SC_NC, 0, sizeof(unsigned long long), s));
+    if (first_event) HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+    if (first_event)
+        hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, rb, re,
+                           key_c, rec_c, sc + SC_NC, sc + SC_FIRST_KEY, err);
+    else
+        hipLaunchKernelGGL((k_entries<MODE, false>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, rb, re,
+                           key_c, rec_c, sc + SC_NC, sc + SC_FIRST_KEY, err);
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(rowptr, 0, (K + 1) * sizeof(unsigned long long), s));
+        HIPCHK(c, hipGetLastError());
+        return PFAAI_OK;
     }
+    int bits = 1;
+    while (bits < 32 && ((int64_t)1 << bits) < K) ++bits;
+    const int passes = (bits + 7) / 8;
+    const int64_t ntiles = ceil_div(n, kRsTile);
+    auto* hist = static_cast<uint32_t*>(c->hist.p);
+    auto* hoff = static_cast<unsigned long long*>(c->hoff.p);
+    uint32_t* kin = key_c;
+    uint32_t* vin = nullptr;
+    uint32_t* kout = static_cast<uint32_t*>(c->key_a.p);
+    uint32_t* vout = static_cast<uint32_t*>(c->val_a.p);
+    uint32_t* kalt = static_cast<uint32_t*>(c->key_b.p);
+    uint32_t* valt = static_cast<uint32_t*>(c->val_b.p);
+    auto* recs = static_cast<uint2*>(c->recs.p);
+    for (int pass = 0; pass < passes; ++pass) {
+        const int shift = 8 * pass;
+        const bool first = pass == 0, last = pass == passes - 1;
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kRsThreads), 0, s, kin, n, shift, hist, ntiles);
+        int rc = scan_u32(c, hist, kRsBins * ntiles, hoff, s);
+        if (rc) return rc;
+#define RS(F, L)                                                                                                  \
+    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, ntiles, \
+                       kout, vout, rec_c, recs)
+        if (first && last) RS(true, true);
+        else if (first) RS(true, false);
+        else if (last) RS(false, true);
+        else RS(false, false);
+#undef RS
+        // ping-pong (never back into key_c, the entries' own buffer)
+        kin = kout;
+        vin = vout;
+        std::swap(kout, kalt);
+        std::swap(vout, valt);
+    }
+    const uint32_t* ksorted = kin;
+    hipLaunchKernelGGL(k_rowptr, dim3(ceil_div(n, 256)), dim3(256), 0, s, ksorted, n, K, rowptr);
     HIPCHK(c, hipGetLastError());
+    return PFAAI_OK;
+}
+
+// Work-list build from the genome-major view (no sort): run table, lengths,
+// scan, one binary search per entry.
+template <int MODE>
+int build_records_g(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool first_event) {
+    const int64_t P = c->prob.n_prot;
+    const int64_t K = (re - rb) * P;
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
+    auto* len = static_cast<uint32_t*>(c->lens.p);
+    HIPCHK(c, hipMemsetAsync(c->blk.p, 0, c->blk.bytes, s));
+    hipLaunchKernelGGL(k_blk, dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, err);
+    if (first_event) {  // lexicographically first E triple, all rows (row Z)
+        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
+                           (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
+                           sc + SC_NC, sc + SC_FIRST_KEY, err);
+    }
+    hipLaunchKernelGGL(k_glen, dim3(ceil_div(K, 256)), dim3(256), 0, s, c->dev, rb, K, len);
+    int rc = scan_u32(c, len, K, rowptr, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_recs_g<MODE>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+                       static_cast<uint2*>(c->recs.p));
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_OK;
+}
+
+int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s) {
+    auto* sums = static_cast<unsigned long long*>(c->sums.p);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kScanTile));
+    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kScanThreads), 0, s, in, n, out, sums);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, s, sums, tiles, sc + SC_GRAND);
+    hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, s, out, n, sums, sc + SC_GRAND,
+                       static_cast<unsigned long long*>(nullptr));
     return PFAAI_OK;
 }
 
@@ -148,10 +226,17 @@ void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t
                     double* aji, double* S, int32_t* N, hipStream_t s) {
     const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    hipLaunchKernelGGL((k_rows<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                       static_cast<const unsigned long long*>(c->rowptr.p),
-                       static_cast<const uint2*>(c->recs.p), chunk, flags, sc + SC_FIRST_KEY, aji, S, N,
-                       sc + SC_EVENTS);
+    auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
+    auto* recs = static_cast<const uint2*>(c->recs.p);
+    if (c->occupancy == 2)
+        hipLaunchKernelGGL((k_rows<MODE, KW, 2>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 3)
+        hipLaunchKernelGGL((k_rows<MODE, KW, 3>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else
+        hipLaunchKernelGGL((k_rows<MODE, KW, 1>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
 template <int MODE>
@@ -187,7 +272,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     c->ev1 = ev[1];
     c->ev2 = ev[2];
     HIPCHK(c, hipEventRecord(c->ev0, s));
-    int rc = build_records<MODE>(c, rb, re, s, compat);
+    int rc = c->has_g ? build_records_g<MODE>(c, rb, re, s, compat) : build_records<MODE>(c, rb, re, s, compat);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
@@ -230,8 +315,9 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->cnt, &c->rowptr, &c->cursor,
-                      &c->recs, &c->sums, &c->scalars, &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
+                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -338,6 +424,22 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     if ((rc = upload(c, c->tcol_row, tcol_row.data(), ni))) return rc;
     if ((rc = upload(c, c->tcol_col, tcol_col.data(), ni))) return rc;
 
+    c->has_g = p.G_off && p.G_tet;
+    if (c->has_g) {
+        const int64_t ng = (int64_t)ni * p.n_prot;
+        if (p.G_off[0] != 0) return fail(c, PFAAI_ERR_INVALID, "G_off must start at 0");
+        for (int64_t k = 0; k < ng; ++k)
+            if (p.G_off[k + 1] < p.G_off[k]) return fail(c, PFAAI_ERR_INVALID, "G_off must be non-decreasing");
+        const int64_t gt = p.G_off[ng];
+        if (gt >= ((int64_t)1 << 32)) return fail(c, PFAAI_ERR_INVALID, "G too large");
+        for (int64_t k = 0; k < gt; ++k)
+            if (p.G_tet[k] < 0 || p.G_tet[k] >= PFAAI_NTETRAMERS)
+                return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
+        if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
+        if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
+        if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint2)))) return rc;
+    }
+
     Dev& d = c->dev;
     d.mode = p.mode;
     d.n_ids = ni;
@@ -357,41 +459,47 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     d.row_genome = static_cast<const int32_t*>(c->row_genome.p);
     d.tcol_row = static_cast<const int32_t*>(c->tcol_row.p);
     d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
+    d.G_off = c->has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
+    d.G_tet = c->has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
+    d.blk = c->has_g ? static_cast<uint2*>(c->blk.p) : nullptr;
 
-    // Work space sized for all rows, so pfaai_run never allocates or syncs:
-    // one counting pass over every row gives the exact record capacity.
-    const int64_t n = c->n_rows * p.n_prot;
-    const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kScanTile));
-    if ((rc = ensure(c, c->cnt, n * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->rowptr, (n + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->cursor, (n + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->sums, tiles * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->recs, 8))) return rc;
-    HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
+    // Work space sized for all rows, so pfaai_run never allocates or syncs.
+    // Work-list entries of a row = F entries of its genome (counted here).
     {
-        auto* cnt = static_cast<uint32_t*>(c->cnt.p);
-        auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-        HIPCHK(c, hipMemsetAsync(cnt, 0, n * sizeof(uint32_t), c->stream));
-        const int64_t rb = 0, re = c->n_rows;
-        switch (p.mode) {
-            case 0: hipLaunchKernelGGL((k_tetra_records<0, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
-            case 1: hipLaunchKernelGGL((k_tetra_records<1, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
-            default: hipLaunchKernelGGL((k_tetra_records<2, 0>), dim3(kNTetramers), dim3(kTetraThreads), 0, c->stream, d, rb, re, cnt, nullptr, nullptr, nullptr, reinterpret_cast<int*>(sc + SC_ERR)); break;
+        std::vector<int64_t> fcount(ni, 0);
+        for (int64_t i = 0; i < p.n_f; ++i) {
+            const int32_t g = p.F_genome[i];
+            if (g < 0 || g >= ni) return fail(c, PFAAI_ERR_INVALID, "F holds a genome id outside [0, n_ids)");
+            fcount[g]++;
         }
-        auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
-        auto* sums = static_cast<unsigned long long*>(c->sums.p);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kScanThreads), 0, c->stream, cnt, n, rowptr, sums);
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, c->stream, sums, tiles, sc + SC_GRAND);
-        hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, c->stream, rowptr, n, sums,
-                           sc + SC_GRAND, static_cast<unsigned long long*>(nullptr));
-        HIPCHK(c, hipGetLastError());
-        unsigned long long host_sc[SC_N];
-        HIPCHK(c, hipMemcpyAsync(host_sc, sc, sizeof(host_sc), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (host_sc[SC_ERR]) return fail(c, PFAAI_ERR_INVALID, "a tetramer block holds more than 4096 protein runs");
-        c->recs_cap = host_sc[SC_GRAND];
-        if ((rc = ensure(c, c->recs, std::max<uint64_t>(1, c->recs_cap) * sizeof(uint2)))) return rc;
+        c->row_fprefix.assign(c->n_rows + 1, 0);
+        for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
+        if (c->has_g) {  // work lists follow G (one record per G entry of a row genome)
+            for (int64_t r = 0; r < c->n_rows; ++r) {
+                const int64_t g0 = (int64_t)c->row_genome_h[r] * p.n_prot;
+                c->row_fprefix[r + 1] = c->row_fprefix[r] + (p.G_off[g0 + p.n_prot] - p.G_off[g0]);
+            }
+        }
     }
+    const int64_t nmax = std::max<int64_t>(1, c->row_fprefix[c->n_rows]);
+    const int64_t K = c->n_rows * p.n_prot;
+    const int64_t ntiles = ceil_div(nmax, kRsTile);
+    const int64_t hist_n = kRsBins * ntiles;
+    if ((rc = ensure(c, c->rowptr, (K + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->lens, std::max<int64_t>(K, 1) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->key_c, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->rec_c, nmax * sizeof(uint2)))) return rc;
+    if ((rc = ensure(c, c->key_a, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->key_b, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->val_a, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->val_b, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->recs, nmax * sizeof(uint2)))) return rc;
+    if ((rc = ensure(c, c->hist, hist_n * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->hoff, (hist_n + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max(hist_n, K), kScanTile)) *
+                                     sizeof(unsigned long long))))
+        return rc;
+    HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
     c->loaded = true;
     return PFAAI_OK;
 }
@@ -436,6 +544,10 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     if (!aji && !S && !N) return fail(c, PFAAI_ERR_INVALID, "no output");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    if (const char* occ = getenv("PFAAI_ROWS_OCC")) {  // tuning knob (A/B of k_rows variants)
+        const int v = atoi(occ);
+        c->occupancy = (v == 1 || v == 3) ? v : 2;
+    }
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
         HIPCHK(c, hipStreamSynchronize(s));
         c->pool_used = 0;
@@ -533,15 +645,21 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
     auto* out = static_cast<int32_t*>(c->dbg.p);
     switch (p.mode) {
         case 0:
-            if ((rc = build_records<0>(c, row, row + 1, c->stream, false))) return rc;
+            if ((rc = c->has_g ? build_records_g<0>(c, row, row + 1, c->stream, false)
+                               : build_records<0>(c, row, row + 1, c->stream, false)))
+                return rc;
             hipLaunchKernelGGL(k_row_counts<0>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;
         case 1:
-            if ((rc = build_records<1>(c, row, row + 1, c->stream, false))) return rc;
+            if ((rc = c->has_g ? build_records_g<1>(c, row, row + 1, c->stream, false)
+                               : build_records<1>(c, row, row + 1, c->stream, false)))
+                return rc;
             hipLaunchKernelGGL(k_row_counts<1>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;
         default:
-            if ((rc = build_records<2>(c, row, row + 1, c->stream, false))) return rc;
+            if ((rc = c->has_g ? build_records_g<2>(c, row, row + 1, c->stream, false)
+                               : build_records<2>(c, row, row + 1, c->stream, false)))
+                return rc;
             hipLaunchKernelGGL(k_row_counts<2>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;
     }

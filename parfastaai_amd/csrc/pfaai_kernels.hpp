@@ -5,12 +5,12 @@
 // (psort.hpp:27-53, 86 % of its wall time) and walks the sorted runs
 // (algorithm_impl.hpp:123-277).  Here E is never built and nothing is sorted:
 //
-//   K-W  k_tetra_records  one workgroup per tetramer block of F: finds the
-//        (tetramer, protein) runs with a wavefront ballot + prefix count,
-//        then turns every F entry whose genome is an output row into
-//        "member ranges" [lo, hi) of that run (the genomes it pairs with),
-//        bucketed per (row, protein) by a counting sort (pass 0 counts,
-//        exclusive scan, pass 1 fills).
+//   K-W  k_entries + k_rs_* + k_rowptr: one workgroup per tetramer block of
+//        F finds the (tetramer, protein) runs with a wavefront ballot +
+//        prefix count and turns every F entry whose genome is an output row
+//        into a "member range" [lo, hi) of its run (the genomes it pairs
+//        with), keyed by (row, protein); a hand-written stable LSD radix
+//        sort groups them per (row, protein) and rowptr marks the groups.
 //   K-S+J k_rows          one workgroup per output row (genome A): for each
 //        protein in ascending order, scatters +1 into an LDS row of packed
 //        u16 intersection counters for every member B of every range
@@ -35,8 +35,6 @@ constexpr int kMaxRuns = 4096;          // proteins per tetramer block (checked 
 constexpr int kRowThreads = 1024;       // K-S+J workgroup (16 waves)
 constexpr int kGroup = 16;              // lanes per member range in the scatter
 constexpr int kNumGroups = kRowThreads / kGroup;
-constexpr uint32_t kRangeMax = 64;      // members per range (longer runs are split)
-constexpr uint32_t kFilterBit = 0x80000000u;
 
 // Device view of a loaded problem (pfaai_problem + derived maps).
 struct Dev {
@@ -53,6 +51,9 @@ struct Dev {
     const int32_t* row_genome;  // [n_rows] genome id of an output row
     const int32_t* tcol_row;    // [n_ids] T column used when the genome is genomeA
     const int32_t* tcol_col;    // [n_ids] T column used when the genome is genomeB
+    const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
+    const int32_t* G_tet;
+    uint2* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run [start, end)
 };
 
 // ---------------------------------------------------------------------------
@@ -97,33 +98,151 @@ __device__ __forceinline__ int64_t lower_bound_g(const int32_t* Fg, int64_t lo, 
     return lo;
 }
 
-__device__ __forceinline__ uint32_t n_pieces(int64_t len) {
-    return len <= 0 ? 0u : (uint32_t)((len + kRangeMax - 1) / kRangeMax);
-}
-
 // ---------------------------------------------------------------------------
-// K-W: member-range work lists per (row, protein).
-//   PASS 0: cnt[(row-row_begin)*P + p] += #ranges
-//   PASS 1: recs[cursor[...]++] = {lo, hi | filter}
-//   PASS 2: first_key = min over all events of (gA, gB, p)  (ref-compat row Z)
+// K-W1: work-list entries.  One workgroup per tetramer block of F: the
+// (tetramer, protein) run heads are found with a wavefront ballot + prefix
+// count and kept in LDS; every F entry whose genome is an output row in
+// [row_begin, row_end) becomes one entry
+//      key = (row - row_begin) * P + protein,  rec = member range [lo, hi)
+//   ALL  : [i+1, run end)              -- partners B > A (ds_impl.hpp:90-92)
+//   QSUB : [run start, run end)        -- filtered per member at scatter time
+//   QT   : [run start, first query)    -- target partners (ds_impl.hpp:421-423)
+// compacted with one global atomic per 256 entries.  FIRST also finds the
+// lexicographically first E triple (gA, gB, p) over all rows (ref-compat row
+// Z).
 // ---------------------------------------------------------------------------
-template <int MODE, int PASS>
-__global__ __launch_bounds__(kTetraThreads) void k_tetra_records(
-    Dev d, int64_t row_begin, int64_t row_end, uint32_t* __restrict__ cnt,
-    unsigned long long* __restrict__ cursor, uint2* __restrict__ recs,
-    unsigned long long* __restrict__ first_key, int* __restrict__ err) {
+template <int MODE, bool FIRST>
+__global__ __launch_bounds__(kTetraThreads) void k_entries(
+    Dev d, int64_t row_begin, int64_t row_end, uint32_t* __restrict__ key_c, uint2* __restrict__ rec_c,
+    unsigned long long* __restrict__ n_c, unsigned long long* __restrict__ first_key, int* __restrict__ err) {
     __shared__ int32_t runs[kMaxRuns + 1];
     __shared__ int32_t wave_cnt[kTetraThreads / 64];
     __shared__ int32_t n_runs;
+    __shared__ unsigned long long chunk_base;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int P = d.n_prot;
+    const unsigned long long lt = (1ull << lane) - 1ull;
 
     for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
         const int64_t s = d.Lp[t], e = d.Lp[t + 1];
         if (s >= e) continue;  // uniform
         if (tid == 0) n_runs = 0;
         __syncthreads();
-        // (t, p) run heads, compacted in order: ballot per wave + wave prefix.
+        for (int64_t base = s; base < e; base += kTetraThreads) {
+            const int64_t i = base + tid;
+            bool head = false;
+            if (i < e) head = (i == s) || (d.Fp[i] != d.Fp[i - 1]);
+            const unsigned long long m = __ballot(head);
+            if (lane == 0) wave_cnt[wid] = __popcll(m);
+            __syncthreads();
+            int off = n_runs;
+            for (int w = 0; w < wid; ++w) off += wave_cnt[w];
+            if (head) {
+                const int pos = off + __popcll(m & lt);
+                if (pos < kMaxRuns) runs[pos] = (int32_t)(i - s);
+                else atomicOr(err, 1);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int add = 0;
+                for (int w = 0; w < kTetraThreads / 64; ++w) add += wave_cnt[w];
+                n_runs += add;
+            }
+            __syncthreads();
+        }
+        const int nr = min(n_runs, kMaxRuns);
+        if (tid == 0) runs[nr] = (int32_t)(e - s);
+        __syncthreads();
+
+        for (int64_t base = s; base < e; base += kTetraThreads) {  // uniform trip count
+            const int64_t i = base + tid;
+            bool valid = false;
+            uint32_t key = 0;
+            uint2 rec = make_uint2(0u, 0u);
+            if (i < e) {
+                const int32_t a = d.Fg[i];
+                const int32_t row = d.row_of[a];
+                if (row >= 0) {
+                    const int32_t rel = (int32_t)(i - s);
+                    int lo = 0, hi = nr;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (runs[mid] <= rel) lo = mid + 1; else hi = mid;
+                    }
+                    const int64_t bs = s + runs[lo - 1], be = s + runs[lo];
+                    const int32_t p = d.Fp[i];
+                    int64_t rlo, rhi;
+                    if constexpr (MODE == 0) { rlo = i + 1; rhi = be; }
+                    else if constexpr (MODE == 1) { rlo = bs; rhi = be; }
+                    else { rlo = bs; rhi = lower_bound_g(d.Fg, bs, be, d.n_tgt); }
+                    rec = make_uint2((uint32_t)rlo, (uint32_t)rhi);
+                    if (row >= row_begin && row < row_end) {
+                        valid = true;
+                        key = (uint32_t)((row - row_begin) * P + p);
+                    }
+                    if constexpr (FIRST) {  // smallest valid partner of A in this run
+                        int32_t b = -1;
+                        if constexpr (MODE == 0) {
+                            if (i + 1 < be) b = d.Fg[i + 1];
+                        } else if constexpr (MODE == 2) {
+                            if (rhi > rlo) b = d.Fg[rlo];
+                        } else {
+                            for (int64_t j = bs; j < be; ++j) {
+                                const int32_t g = d.Fg[j];
+                                if (j != i && (!d.is_q[g] || g > a)) { b = g; break; }
+                            }
+                        }
+                        if (b >= 0)
+                            atomicMin(first_key, ((unsigned long long)a << 42) | ((unsigned long long)b << 21) |
+                                                     (unsigned long long)p);
+                    }
+                }
+            }
+            // order-free compaction: one global atomic per 256 entries
+            const unsigned long long m = __ballot(valid);
+            if (lane == 0) wave_cnt[wid] = __popcll(m);
+            __syncthreads();
+            if (tid == 0) {
+                int tot = 0;
+                for (int w = 0; w < kTetraThreads / 64; ++w) tot += wave_cnt[w];
+                chunk_base = tot ? atomicAdd(n_c, (unsigned long long)tot) : 0ull;
+            }
+            __syncthreads();
+            if (valid) {
+                unsigned long long off = chunk_base + __popcll(m & lt);
+                for (int w = 0; w < wid; ++w) off += wave_cnt[w];
+                key_c[off] = key;
+                rec_c[off] = rec;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K-W1g (genome-major input): run table + work lists without any sort.
+//   k_blk:    one workgroup per tetramer block: run heads by wavefront ballot,
+//             blk[p * 160000 + t] = [start, end) of run (t, p) in F.
+//   k_glen:   work-list length of every (row, protein) = its G list length.
+//   k_recs_g: one workgroup per output row; each G entry (A, p, t) of the
+//             row looks up its run and becomes the member range of A in it:
+//               ALL  [pos(A)+1, end)   pos(A) by binary search of the run's
+//                                      sorted genome ids
+//               QSUB [start, end)      (filtered per member at scatter time)
+//               QT   [start, first query)
+//             written at rowptr[(row, p)] + its rank in the G list, so the
+//             lists come out grouped per (row, protein) with no atomics.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int* __restrict__ err) {
+    __shared__ int32_t runs[kMaxRuns + 1];
+    __shared__ int32_t wave_cnt[kTetraThreads / 64];
+    __shared__ int32_t n_runs;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
+        const int64_t s = d.Lp[t], e = d.Lp[t + 1];
+        if (s >= e) continue;
+        if (tid == 0) n_runs = 0;
+        __syncthreads();
         for (int64_t base = s; base < e; base += kTetraThreads) {
             const int64_t i = base + tid;
             bool head = false;
@@ -149,67 +268,198 @@ __global__ __launch_bounds__(kTetraThreads) void k_tetra_records(
         const int nr = min(n_runs, kMaxRuns);
         if (tid == 0) runs[nr] = (int32_t)(e - s);
         __syncthreads();
+        for (int j = tid; j < nr; j += kTetraThreads) {
+            const int64_t rs = s + runs[j], re = s + runs[j + 1];
+            d.blk[(int64_t)d.Fp[rs] * kNTetramers + t] = make_uint2((uint32_t)rs, (uint32_t)re);
+        }
+        __syncthreads();
+    }
+}
 
-        for (int64_t i = s + tid; i < e; i += kTetraThreads) {
-            const int32_t a = d.Fg[i];
-            const int32_t row = d.row_of[a];
-            if (row < 0) continue;
-            if (PASS != 2 && (row < row_begin || row >= row_end)) continue;
-            // run containing i: last head <= i - s
-            const int32_t rel = (int32_t)(i - s);
-            int lo = 0, hi = nr;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (runs[mid] <= rel) lo = mid + 1; else hi = mid;
+__global__ void k_glen(Dev d, int64_t row_begin, int64_t n_keys, uint32_t* __restrict__ len) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    const int64_t r = row_begin + k / d.n_prot, p = k % d.n_prot;
+    const int64_t gp = (int64_t)d.row_genome[r] * d.n_prot + p;
+    len[k] = (uint32_t)(d.G_off[gp + 1] - d.G_off[gp]);
+}
+
+// Each thread walks kRecsBatch entries at once: their G, run-table and
+// binary-search loads are issued together (8 independent chains in flight
+// per lane) -- the kernel is bound by dependent-load latency otherwise.
+constexpr int kRecsBatch = 8;
+
+template <int MODE>
+__global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_begin,
+                                                          const unsigned long long* __restrict__ rowptr,
+                                                          uint2* __restrict__ recs) {
+    __shared__ long long goff[kMaxRuns + 1];
+    const int tid = threadIdx.x;
+    const int64_t rl = blockIdx.x;
+    const int32_t a = d.row_genome[row_begin + rl];
+    const int P = d.n_prot;
+    const int64_t g0 = (int64_t)a * P;
+    for (int p = tid; p <= P; p += kTetraThreads) goff[p] = d.G_off[g0 + p];
+    __syncthreads();
+    const int64_t k0 = goff[0], k1 = goff[P];
+    for (int64_t kb = k0 + tid; kb < k1; kb += (int64_t)kTetraThreads * kRecsBatch) {
+        int pr[kRecsBatch];
+        uint32_t lo[kRecsBatch], hi[kRecsBatch], end[kRecsBatch];
+        bool live[kRecsBatch];
+#pragma unroll
+        for (int u = 0; u < kRecsBatch; ++u) {
+            const int64_t k = kb + (int64_t)u * kTetraThreads;
+            live[u] = k < k1;
+            int plo = 0, phi = P;  // protein of entry k: last p with goff[p] <= k
+            while (phi - plo > 1) {
+                const int mid = (plo + phi) >> 1;
+                if (goff[mid] <= k) plo = mid; else phi = mid;
             }
-            const int64_t bs = s + runs[lo - 1], be = s + runs[lo];
-            const int32_t p = d.Fp[i];
-            // member ranges of this entry (the valid partners in its run)
-            int64_t r0lo = 0, r0hi = 0, r1lo = 0, r1hi = 0;  // r0 may carry the filter bit
-            if constexpr (MODE == 0) {
-                r1lo = i + 1; r1hi = be;
-            } else if constexpr (MODE == 1) {
-                r0lo = bs; r0hi = i;      // members before a: valid iff non-query
-                r1lo = i + 1; r1hi = be;  // members after a: always valid
-            } else {
-                r0lo = bs; r0hi = lower_bound_g(d.Fg, bs, be, d.n_tgt);  // targets
-            }
-            if constexpr (PASS == 0) {
-                const uint32_t np = n_pieces(r0hi - r0lo) + n_pieces(r1hi - r1lo);
-                if (np) atomicAdd(&cnt[(int64_t)(row - row_begin) * P + p], np);
-            } else if constexpr (PASS == 1) {
-                const uint32_t n0 = n_pieces(r0hi - r0lo), n1 = n_pieces(r1hi - r1lo);
-                if (n0 + n1 == 0) continue;
-                unsigned long long k =
-                    atomicAdd(&cursor[(int64_t)(row - row_begin) * P + p], (unsigned long long)(n0 + n1));
-                const uint32_t f0 = (MODE == 1) ? kFilterBit : 0u;
-                for (int64_t x = r0lo; x < r0hi; x += kRangeMax, ++k)
-                    recs[k] = make_uint2((uint32_t)x, (uint32_t)min(r0hi, x + (int64_t)kRangeMax) | f0);
-                for (int64_t x = r1lo; x < r1hi; x += kRangeMax, ++k)
-                    recs[k] = make_uint2((uint32_t)x, (uint32_t)min(r1hi, x + (int64_t)kRangeMax));
-            } else {
-                // smallest valid partner of a in this run
-                int32_t b = -1;
-                if constexpr (MODE == 0) {
-                    if (i + 1 < be) b = d.Fg[i + 1];
-                } else if constexpr (MODE == 2) {
-                    if (r0hi > r0lo) b = d.Fg[r0lo];
-                } else {
-                    for (int64_t j = bs; j < be; ++j) {
-                        const int32_t g = d.Fg[j];
-                        if (j != i && (!d.is_q[g] || g > a)) { b = g; break; }
-                    }
+            pr[u] = plo;
+        }
+        int32_t t[kRecsBatch];
+#pragma unroll
+        for (int u = 0; u < kRecsBatch; ++u) t[u] = live[u] ? d.G_tet[kb + (int64_t)u * kTetraThreads] : 0;
+#pragma unroll
+        for (int u = 0; u < kRecsBatch; ++u) {
+            const uint2 run = live[u] ? d.blk[(int64_t)pr[u] * kNTetramers + t[u]] : make_uint2(0u, 0u);
+            lo[u] = run.x;
+            hi[u] = run.y;
+            end[u] = run.y;
+            live[u] = live[u] && run.y > run.x;
+        }
+        if constexpr (MODE != 1) {
+            // lockstep lower_bound of A (ALL) or of n_tgt (QT) in each run's sorted genome ids
+            const int32_t key = MODE == 0 ? a : d.n_tgt;
+            bool any = true;
+            while (any) {
+                any = false;
+                int32_t v[kRecsBatch];
+                uint32_t mid[kRecsBatch];
+#pragma unroll
+                for (int u = 0; u < kRecsBatch; ++u) {
+                    mid[u] = (lo[u] + hi[u]) >> 1;
+                    v[u] = (live[u] && lo[u] < hi[u]) ? d.Fg[mid[u]] : 0;
                 }
-                if (b >= 0) {
-                    const unsigned long long key = ((unsigned long long)a << 42) |
-                                                   ((unsigned long long)b << 21) |
-                                                   (unsigned long long)p;
-                    atomicMin(first_key, key);
+#pragma unroll
+                for (int u = 0; u < kRecsBatch; ++u) {
+                    if (live[u] && lo[u] < hi[u]) {
+                        if (v[u] < key) lo[u] = mid[u] + 1; else hi[u] = mid[u];
+                        any |= lo[u] < hi[u];
+                    }
                 }
             }
         }
-        __syncthreads();  // runs[] is reused by the next tetramer
+#pragma unroll
+        for (int u = 0; u < kRecsBatch; ++u) {
+            const int64_t k = kb + (int64_t)u * kTetraThreads;
+            if (k >= k1) continue;
+            uint2 rec = make_uint2(0u, 0u);
+            if (live[u]) {
+                if constexpr (MODE == 0) {
+                    if (lo[u] < end[u] && d.Fg[lo[u]] == a) rec = make_uint2(lo[u] + 1u, end[u]);
+                } else if constexpr (MODE == 1) {
+                    rec = make_uint2(lo[u], end[u]);
+                } else {
+                    const uint2 run = d.blk[(int64_t)pr[u] * kNTetramers + t[u]];
+                    rec = make_uint2(run.x, lo[u]);
+                }
+            }
+            recs[rowptr[rl * P + pr[u]] + (k - goff[pr[u]])] = rec;
+        }
     }
+}
+
+// ---------------------------------------------------------------------------
+// K-W2: stable LSD radix sort of the (key, entry) pairs, 8-bit digits.
+// Tiles of 4096 keys (256 threads x 16, striped so loads coalesce).  Per
+// pass: k_rs_hist (LDS histogram per tile -> hist[digit][tile]), an
+// exclusive scan of hist (digit-major: global base of every (digit, tile)),
+// k_rs_scatter (stable in-tile rank: per 256-key round, peers with the same
+// digit found with 8 wavefront ballots, wave counts prefixed in LDS).  The
+// last pass writes the final work list rec_c[entry] at the sorted position.
+// ---------------------------------------------------------------------------
+constexpr int kRsThreads = 256;
+constexpr int kRsRounds = 16;
+constexpr int kRsTile = kRsThreads * kRsRounds;
+constexpr int kRsBins = 256;
+
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                        uint32_t* __restrict__ hist, int64_t ntiles) {
+    __shared__ uint32_t h[kRsBins];
+    const int tid = threadIdx.x;
+    h[tid] = 0u;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+#pragma unroll 4
+    for (int r = 0; r < kRsRounds; ++r) {
+        const int64_t j = base + r * kRsThreads + tid;
+        if (j < n) atomicAdd(&h[(keys[j] >> shift) & (kRsBins - 1)], 1u);
+    }
+    __syncthreads();
+    hist[(int64_t)tid * ntiles + blockIdx.x] = h[tid];
+}
+
+template <bool FIRSTPASS, bool LAST>
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int64_t n, int shift,
+    const unsigned long long* __restrict__ offs, int64_t ntiles, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, const uint2* __restrict__ rec_c, uint2* __restrict__ recs_out) {
+    __shared__ unsigned long long base[kRsBins];
+    __shared__ unsigned long long wpos[kRsThreads / 64][kRsBins];
+    __shared__ uint32_t wcnt[kRsThreads / 64][kRsBins];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    base[tid] = offs[(int64_t)tid * ntiles + blockIdx.x];
+    const int64_t t0 = (int64_t)blockIdx.x * kRsTile;
+    for (int r = 0; r < kRsRounds; ++r) {
+        const int64_t j = t0 + r * kRsThreads + tid;
+        const bool valid = j < n;
+        const uint32_t k = valid ? keys_in[j] : 0u;
+        const uint32_t v = valid ? (FIRSTPASS ? (uint32_t)j : vals_in[j]) : 0u;
+        const uint32_t dig = (k >> shift) & (kRsBins - 1);
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool on = (dig >> bit) & 1u;
+            const unsigned long long m = __ballot(on);
+            peers &= on ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+#pragma unroll
+        for (int w = 0; w < kRsThreads / 64; ++w) wcnt[w][tid] = 0u;
+        __syncthreads();
+        if (valid && rank == 0) wcnt[wid][dig] = __popcll(peers);
+        __syncthreads();
+        {  // digit tid: exclusive prefix over waves, advance the running base
+            unsigned long long run = base[tid];
+#pragma unroll
+            for (int w = 0; w < kRsThreads / 64; ++w) {
+                wpos[w][tid] = run;
+                run += wcnt[w][tid];
+            }
+            base[tid] = run;
+        }
+        __syncthreads();
+        if (valid) {
+            const unsigned long long pos = wpos[wid][dig] + rank;
+            keys_out[pos] = k;
+            if (LAST) recs_out[pos] = rec_c[v];
+            else vals_out[pos] = v;
+        }
+    }
+}
+
+// rowptr[k] = first sorted position with key >= k  (k in [0, K]).
+__global__ void k_rowptr(const uint32_t* __restrict__ keys, int64_t n, int64_t K,
+                         unsigned long long* __restrict__ rowptr) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t k = keys[j];
+    const int64_t kp = j > 0 ? (int64_t)keys[j - 1] : -1;
+    for (int64_t x = kp + 1; x <= k; ++x) rowptr[x] = (unsigned long long)j;
+    if (j == n - 1)
+        for (int64_t x = k + 1; x <= K; ++x) rowptr[x] = (unsigned long long)n;
 }
 
 // ---------------------------------------------------------------------------
@@ -305,28 +555,74 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_add(unsigned long long* _
 // ---------------------------------------------------------------------------
 // K-S: scatter the E triples (p, A, *) of one row and protein into LDS
 // counters.  acc word w holds columns cc0+2w (low u16) and cc0+2w+1 (high).
-// Each 16-lane group walks one member range (<= 64 genome ids, contiguous in
-// F, so each group load is one 64-B segment).
+// The (row, protein) member ranges are first staged in LDS with one
+// coalesced load; then each 16-lane group takes kUnroll ranges at a time and
+// issues their first member loads together (kUnroll independent 64-B loads
+// in flight per group, 256 per workgroup) before the LDS atomics -- the
+// scatter is bound by load latency, so memory-level parallelism is the lever.
+// Ranges hold <= 64 members (longer runs are split at build time).
 // ---------------------------------------------------------------------------
 template <int MODE>
-__device__ __forceinline__ uint32_t scatter_row_protein(const Dev& d, const uint2* __restrict__ recs,
+__device__ __forceinline__ void scatter_one(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0,
+                                            int32_t cc1, uint32_t& ev) {
+    if (b < 0) return;
+    if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
+    if (b >= cc0 && b < cc1) {
+        const uint32_t o = (uint32_t)(b - cc0);
+        atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));
+        ++ev;
+    }
+}
+
+constexpr uint32_t kLongCut = 4 * kGroup;  // a group walks at most this many members of a range
+
+// rec_lds: kRowThreads staged ranges; long_lds: tails of long ranges, walked
+// by the whole workgroup.
+template <int MODE, int kUnroll, bool LONGQ = true>
+__device__ __forceinline__ uint32_t scatter_row_protein(const Dev& d, int32_t a, const uint2* __restrict__ recs,
                                                         uint64_t rb, uint64_t re, uint32_t* acc,
+                                                        uint2* rec_lds, uint2* long_lds, int* n_long,
                                                         int32_t cc0, int32_t cc1) {
     const int tid = threadIdx.x;
     const int grp = tid / kGroup, gl = tid % kGroup;
     uint32_t ev = 0;
-    for (uint64_t k = rb + grp; k < re; k += kNumGroups) {
-        const uint2 r = recs[k];
-        const uint32_t lo = r.x, hi = r.y & ~kFilterBit;
-        const bool filt = (MODE == 1) && (r.y & kFilterBit);
-        for (uint32_t m = lo + gl; m < hi; m += kGroup) {
-            const int32_t b = d.Fg[m];
-            if (MODE == 1 && filt && d.is_q[b]) continue;
-            if (b >= cc0 && b < cc1) {
-                const uint32_t o = (uint32_t)(b - cc0);
-                atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));
-                ++ev;
+    for (uint64_t base = rb; base < re; base += kRowThreads) {  // uniform trip count
+        const int n = (int)((re - base) < (uint64_t)kRowThreads ? (re - base) : (uint64_t)kRowThreads);
+        __syncthreads();  // previous readers of rec_lds / long_lds are done
+        if (tid < n) rec_lds[tid] = recs[base + tid];
+        if (tid == 0) *n_long = 0;
+        __syncthreads();
+        for (int j = grp; j < n; j += kNumGroups * kUnroll) {
+            uint32_t lo[kUnroll], hi[kUnroll];
+            int32_t b[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int k = j + u * kNumGroups;
+                const uint2 r = k < n ? rec_lds[k] : make_uint2(0u, 0u);
+                lo[u] = r.x;
+                hi[u] = r.y;
             }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) b[u] = lo[u] + gl < hi[u] ? d.Fg[lo[u] + gl] : -1;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) scatter_one<MODE>(d, a, b[u], acc, cc0, cc1, ev);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint32_t cut = (LONGQ && hi[u] - lo[u] > kLongCut) ? lo[u] + kLongCut : hi[u];
+                for (uint32_t m = lo[u] + kGroup + gl; m < cut; m += kGroup)
+                    scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
+                if (cut < hi[u] && gl == 0) {  // hand the tail to the whole workgroup
+                    const int slot = atomicAdd(n_long, 1);
+                    long_lds[slot] = make_uint2(cut, hi[u]);
+                }
+            }
+        }
+        if (!LONGQ) continue;
+        __syncthreads();
+        const int nl = *n_long;
+        for (int q = 0; q < nl; ++q) {  // e.g. a core tetramer shared by every genome
+            const uint2 r = long_lds[q];
+            for (uint32_t m = r.x + tid; m < r.y; m += kRowThreads) scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
         }
     }
     return ev;
@@ -343,13 +639,19 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // counter words w = t + k*1024 (k < KW), i.e. columns cc0+2w, cc0+2w+1, and
 // keeps their S (fp64) and N (packed u16) in registers across all proteins.
 // ---------------------------------------------------------------------------
-template <int MODE, int KW>
-__global__ __launch_bounds__(kRowThreads) void k_rows(
+// OCC = 2: two workgroups per CU (<= 64 VGPRs), 4 ranges in flight per group;
+// OCC = 1: one workgroup per CU, 8 ranges in flight per group;
+// OCC = 3: as 2, but long ranges are walked by their group alone.
+template <int MODE, int KW, int OCC>
+__global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
     const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
     const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
     unsigned long long* __restrict__ n_events) {
     extern __shared__ uint32_t acc[];
+    __shared__ uint2 rec_lds[kRowThreads];
+    __shared__ uint2 long_lds[kRowThreads];
+    __shared__ int n_long;
     const int tid = threadIdx.x;
     const int64_t rl = blockIdx.x;  // local row
     const int32_t a = d.row_genome[row_begin + rl];
@@ -374,7 +676,8 @@ __global__ __launch_bounds__(kRowThreads) void k_rows(
     for (int p = 0; p < P; ++p) {
         const uint64_t rb = rowptr[rl * P + p], re = rowptr[rl * P + p + 1];
         if (rb == re) continue;  // uniform: no E triple (p, a, *)
-        ev += scatter_row_protein<MODE>(d, recs, rb, re, acc, cc0, cc1);
+        ev += scatter_row_protein<MODE, OCC == 1 ? 8 : 4, OCC != 3>(d, a, recs, rb, re, acc, rec_lds, long_lds,
+                                                                    &n_long, cc0, cc1);
         __syncthreads();
         const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
         const int32_t ta = Tp[tca];
@@ -440,6 +743,9 @@ __global__ __launch_bounds__(kRowThreads) void k_row_counts(
     Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
     const uint2* __restrict__ recs, int32_t chunk_cols, int32_t* __restrict__ counts) {
     extern __shared__ uint32_t acc[];
+    __shared__ uint2 rec_lds[kRowThreads];
+    __shared__ uint2 long_lds[kRowThreads];
+    __shared__ int n_long;
     const int tid = threadIdx.x;
     const int32_t a = d.row_genome[row_begin];
     int32_t clo, chi;
@@ -452,7 +758,7 @@ __global__ __launch_bounds__(kRowThreads) void k_row_counts(
     __syncthreads();
     for (int p = 0; p < d.n_prot; ++p) {
         const uint64_t rb = rowptr[p], re = rowptr[p + 1];
-        scatter_row_protein<MODE>(d, recs, rb, re, acc, cc0, cc1);
+        scatter_row_protein<MODE, 4>(d, a, recs, rb, re, acc, rec_lds, long_lds, &n_long, cc0, cc1);
         __syncthreads();
         for (int w = tid; w < ncw; w += kRowThreads) {
             const uint32_t v = acc[w];

@@ -44,6 +44,18 @@ class DataStruct:
         self.protein_set = list(protein_set) if protein_set is not None else [f"P{i}" for i in range(self.n_prot)]
         assert self.Lp[-1] == len(self.F_genome), "Lc does not match |F|"
 
+    G_off = None  # optional genome-major view (the `<p>_genomes` blobs)
+    G_tet = None
+
+    def with_genome_major(self, G_off, G_tet):
+        """Attach the genome-major tetramer lists ((genome, protein)-major CSR)."""
+        self.G_off = np.ascontiguousarray(G_off, dtype=np.int64)
+        self.G_tet = np.ascontiguousarray(G_tet, dtype=np.int32)
+        return self
+
+    def _g(self):
+        return {} if self.G_off is None else dict(G_off=self.G_off, G_tet=self.G_tet)
+
     @classmethod
     def from_split(cls, Lp, F_prot, F_genome, T, *args, **kw):
         """Build from int64 Lp[160001] and separate F columns (no copies of F)."""
@@ -147,7 +159,7 @@ class ParFAAIData(DataStruct):
 
     def problem(self):
         return dict(mode=self.mode, n_ids=self.n_genomes, n_prot=self.n_prot, Lp=self.Lp,
-                    F_prot=self.F_prot, F_genome=self.F_genome, T=self.T)
+                    F_prot=self.F_prot, F_genome=self.F_genome, T=self.T, **self._g())
 
 
 class ParFAAIQSubData(DataStruct):
@@ -232,7 +244,7 @@ class ParFAAIQSubData(DataStruct):
     def problem(self):
         return dict(mode=self.mode, n_ids=self.n_genomes, n_prot=self.n_prot, Lp=self.Lp,
                     F_prot=self.F_prot, F_genome=self.F_genome, T=self.T, n_qry=self.n_qry,
-                    n_tgt=self.n_tgt, is_q=self.is_q, q_index=self.q_index, t_rank=self.t_rank)
+                    n_tgt=self.n_tgt, is_q=self.is_q, q_index=self.q_index, t_rank=self.t_rank, **self._g())
 
 
 class ParFAAIQryTgtData(DataStruct):
@@ -303,4 +315,4 @@ class ParFAAIQryTgtData(DataStruct):
     def problem(self):
         return dict(mode=self.mode, n_ids=self.n_ids, n_prot=self.n_prot, Lp=self.Lp,
                     F_prot=self.F_prot, F_genome=self.F_genome, T=self.T, n_qry=self.n_qry,
-                    n_tgt=self.n_tgt, is_q=self.is_q)
+                    n_tgt=self.n_tgt, is_q=self.is_q, **self._g())

@@ -1,0 +1,148 @@
+// datastruct.hpp -- host mirror of the reference's three DataStructInterface
+// modes (ds_impl.hpp), holding the loader's arrays and the mode's index maps.
+// They expose exactly the accessors pfaai::ParFAAIHipImpl (include/
+// pfaai_hip.hpp) and printOutput need, with the reference's names.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "scp_db.hpp"
+
+namespace pfaai_host {
+
+struct JACTuple {  // JACTuple<int, double>, interface.hpp:61-75
+    int32_t genomeA, genomeB;
+    double S;
+    int32_t N;
+};
+
+class DataBase {
+  public:
+    using JACType = JACTuple;
+    DataBase(DBMetaData meta, LoadedArrays arr) : m_meta(std::move(meta)), m_arr(std::move(arr)) {
+        m_Lp.assign(kNTetramers, 0);
+        int32_t run = 0;
+        for (int t = 0; t < kNTetramers; ++t) {  // parallelPrefixSum, ds_helper.hpp:112-122
+            m_Lp[t] = run;
+            run += m_arr.Lc[t];
+        }
+    }
+    const std::vector<int32_t>& refLc() const { return m_arr.Lc; }
+    const std::vector<int32_t>& refLp() const { return m_Lp; }
+    const std::vector<DPair>& refF() const { return m_arr.F; }
+    const DMatrix& refT() const { return m_arr.T; }
+    const DBMetaData& meta() const { return m_meta; }
+
+  protected:
+    DBMetaData m_meta;
+    LoadedArrays m_arr;
+    std::vector<int32_t> m_Lp;
+};
+
+// ParFAAIData (ds_impl.hpp:38-151)
+class AllData : public DataBase {
+  public:
+    using DataBase::DataBase;
+    int64_t n() const { return (int64_t)m_meta.genomeSet.size(); }
+    const std::vector<std::string>& refQuerySet() const { return m_meta.genomeSet; }
+    const std::vector<std::string>& refTargetSet() const { return m_meta.genomeSet; }
+    int64_t qrySetSize() const { return n(); }
+    int64_t tgtSetSize() const { return n(); }
+    int64_t nGenomePairs() const { return n() * (n() - 1) / 2; }
+    bool isQryGenome(int32_t) const { return true; }
+    int32_t mapQueryId(int32_t g) const { return g; }
+    int32_t mapTargetId(int32_t g) const { return g; }
+    std::vector<JACType> initJAC() const {
+        std::vector<JACType> j(nGenomePairs());
+        int32_t a = 0, b = 1;
+        for (auto& x : j) {
+            x.genomeA = a;
+            x.genomeB = b;
+            x.S = 0.0;
+            x.N = 0;
+            if (b == n() - 1) { ++a; b = a + 1; } else { ++b; }
+        }
+        return j;
+    }
+};
+
+// ParFAAIQSubData (ds_impl.hpp:158-337)
+class QSubData : public DataBase {
+  public:
+    QSubData(DBMetaData meta, LoadedArrays arr, std::vector<std::string> qry)
+        : DataBase(std::move(meta), std::move(arr)), m_qry(std::move(qry)) {
+        const int32_t n = (int32_t)m_meta.genomeSet.size();
+        std::unordered_map<std::string, int32_t> qpos;
+        for (std::size_t i = 0; i < m_qry.size(); ++i) qpos.emplace(m_qry[i], (int32_t)i);
+        m_isq.assign(n, 0);
+        m_map.assign(n, 0);
+        m_qlook.assign(m_qry.size(), 0);
+        for (int32_t ix = 0, jx = 0; ix < n; ++ix) {
+            auto it = qpos.find(m_meta.genomeSet[ix]);
+            if (it != qpos.end()) {
+                m_isq[ix] = 1;
+                m_qlook[it->second] = ix;
+                m_map[ix] = it->second;
+            } else {
+                m_tlook.push_back(ix);
+                m_map[ix] = jx++;
+            }
+        }
+    }
+    const std::vector<std::string>& refQuerySet() const { return m_qry; }
+    const std::vector<std::string>& refTargetSet() const { return m_meta.genomeSet; }
+    int64_t qrySetSize() const { return (int64_t)m_qry.size(); }
+    int64_t tgtSetSize() const { return (int64_t)m_meta.genomeSet.size(); }
+    int64_t nTgt() const { return tgtSetSize() - qrySetSize(); }
+    int64_t nGenomePairs() const { return qrySetSize() * nTgt() + qrySetSize() * (qrySetSize() - 1) / 2; }
+    bool isQryGenome(int32_t g) const { return m_isq[g]; }
+    int32_t mapQueryId(int32_t g) const { return m_map[g]; }
+    int32_t mapTargetId(int32_t g) const { return g; }
+    std::vector<JACType> initJAC() const {
+        std::vector<JACType> j(nGenomePairs(), JACType{0, 0, 0.0, 0});
+        const int64_t qt = qrySetSize() * nTgt();
+        for (int64_t i = 0; i < qt; ++i) {
+            j[i].genomeA = m_qlook[i / nTgt()];
+            j[i].genomeB = m_tlook[i % nTgt()];
+        }
+        int32_t a = 0, b = 1;
+        for (int64_t i = qt; i < (int64_t)j.size(); ++i) {
+            j[i].genomeA = m_qlook[a];
+            j[i].genomeB = m_qlook[b];
+            if (b == qrySetSize() - 1) { ++a; b = a + 1; } else { ++b; }
+        }
+        return j;
+    }
+
+  private:
+    std::vector<std::string> m_qry;
+    std::vector<uint8_t> m_isq;
+    std::vector<int32_t> m_map, m_qlook, m_tlook;
+};
+
+// ParFAAIQryTgtData (ds_impl.hpp:343-490): targets 0..nT-1, queries nT..
+class QTData : public DataBase {
+  public:
+    using DataBase::DataBase;
+    const std::vector<std::string>& refQuerySet() const { return m_meta.qyGenomeSet; }
+    const std::vector<std::string>& refTargetSet() const { return m_meta.genomeSet; }
+    int64_t qrySetSize() const { return (int64_t)m_meta.qyGenomeSet.size(); }
+    int64_t tgtSetSize() const { return (int64_t)m_meta.genomeSet.size(); }
+    int64_t nGenomePairs() const { return qrySetSize() * tgtSetSize(); }
+    bool isQryGenome(int32_t g) const { return g >= tgtSetSize(); }
+    int32_t mapQueryId(int32_t g) const { return g < tgtSetSize() ? g : (int32_t)(g - tgtSetSize()); }
+    int32_t mapTargetId(int32_t g) const { return mapQueryId(g); }
+    // the reference's ids (i/nT, nQ + i%nT), ds_impl.hpp:434-436
+    std::vector<JACType> initJAC() const {
+        std::vector<JACType> j(nGenomePairs(), JACType{0, 0, 0.0, 0});
+        for (int64_t i = 0; i < (int64_t)j.size(); ++i) {
+            j[i].genomeA = (int32_t)(i / tgtSetSize());
+            j[i].genomeB = (int32_t)(qrySetSize() + i % tgtSetSize());
+        }
+        return j;
+    }
+};
+
+}  // namespace pfaai_host

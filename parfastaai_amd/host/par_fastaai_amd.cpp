@@ -1,0 +1,279 @@
+// par_fastaai_amd -- drop-in for the reference CLI `par_fastaai.x`
+// (src/main.cpp:56-356) on the MI355X engine.
+//
+//   par_fastaai_amd [-r query_db] [-s sep] [-q query_list] in_db out_csv
+//                   [--ref-compat] [--device N] [--bin PREFIX]
+//
+// Same options, same mode dispatch (main.cpp:337-356), same validation
+// errors and exit codes (3 for a bad -q list or overlapping -r genomes,
+// main.cpp:204-300; 105 / 106 / 109 for option validation / missing
+// required / unexpected arguments, as CLI11 returns them), same CSV.
+// The AJI hot path runs on the GPU through pfaai::ParFAAIHipImpl
+// (include/pfaai_hip.hpp -> libpfaai_hip.so); SQLite ingest and CSV
+// formatting are parallel host code.
+#include <sys/stat.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "datastruct.hpp"
+#include "output.hpp"
+#include "pfaai_hip.hpp"
+#include "scp_db.hpp"
+
+using namespace pfaai_host;
+
+namespace {
+
+struct AppParams {  // main.cpp:56-131
+    std::string pathToDatabase, pathToQryDatabase, pathToQrySubsetFile, pathToOutputFile;
+    std::string outFieldSeparator = ",";
+    std::string binPrefix;
+    std::vector<std::string> qryGenomeSet;
+    bool refCompat = false;
+    int device = 0;
+
+    void print() const {
+        std::vector<std::string> args = {" Input Database  : " + pathToDatabase + " ",
+                                         " Query Database  : " + pathToQryDatabase + " ",
+                                         " Query Subset    : " + pathToQrySubsetFile + " ",
+                                         " Output File     : " + pathToOutputFile + " ",
+                                         " Field Separator : " + outFieldSeparator + " "};
+        std::size_t w = 0;
+        for (auto& a : args) w = std::max(w, a.size());
+        std::string bar;
+        for (std::size_t i = 0; i < w; ++i) bar += "─";
+        std::cout << " ┌" << bar << "┐\n";
+        for (auto& a : args) std::cout << " │" << a << std::string(w - a.size(), ' ') << "│\n";
+        std::cout << " └" << bar << "┘\n";
+    }
+
+    void load_query_genomes() {  // main.cpp:114-124
+        std::ifstream in(pathToQrySubsetFile);
+        std::string s;
+        while (in >> s) qryGenomeSet.push_back(s);
+    }
+};
+
+bool is_file(const std::string& p) {
+    struct stat st;
+    return stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+const char* kUsage =
+    "MI355X-native ParFastAAI (all-pairs AJI)\n"
+    "Usage: par_fastaai_amd [OPTIONS] path_to_input_db path_to_output_file\n\n"
+    "Positionals:\n"
+    "  path_to_input_db TEXT:FILE REQUIRED   Path to the Input Database\n"
+    "  path_to_output_file TEXT REQUIRED     Path to output csv file.\n\n"
+    "Options:\n"
+    "  -h,--help                Print this help message and exit\n"
+    "  -r,--query_db TEXT:FILE  Path to the Query Database [Optional (default: Same as the Input DB)]\n"
+    "  -s,--separator TEXT [,]  Field Separator in the output file [Optional (default: ,)].\n"
+    "  -q,--query_subset TEXT:FILE  Path to Query List (Should be subset of genomoes in the input DB.)\n"
+    "  --ref-compat             Reproduce the reference's quirks (zero-overlap pairs, QT T indexing)\n"
+    "  --device INT [0]         HIP device\n"
+    "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n";
+
+// CLI11-compatible parse: returns -1 to continue, else the exit code.
+int parse(int argc, char** argv, AppParams& a) {
+    std::vector<std::string> pos, extras;
+    for (int i = 1; i < argc; ++i) {
+        std::string s = argv[i];
+        auto value = [&](std::string& dst) -> bool {
+            auto eq = s.find('=');
+            if (s.rfind("--", 0) == 0 && eq != std::string::npos) {
+                dst = s.substr(eq + 1);
+                return true;
+            }
+            if (i + 1 >= argc) return false;
+            dst = argv[++i];
+            return true;
+        };
+        auto is = [&](const char* sh, const char* lg) {
+            return s == sh || s == lg || (s.rfind(std::string(lg) + "=", 0) == 0);
+        };
+        if (s == "-h" || s == "--help") {
+            std::cout << kUsage;
+            return 0;
+        } else if (is("-r", "--query_db")) {
+            if (!value(a.pathToQryDatabase)) { std::cerr << "--query_db: 1 required TEXT:FILE missing\n"; return 114; }
+        } else if (is("-s", "--separator")) {
+            if (!value(a.outFieldSeparator)) { std::cerr << "--separator: 1 required TEXT missing\n"; return 114; }
+        } else if (is("-q", "--query_subset")) {
+            if (!value(a.pathToQrySubsetFile)) { std::cerr << "--query_subset: 1 required TEXT:FILE missing\n"; return 114; }
+        } else if (s == "--ref-compat") {
+            a.refCompat = true;
+        } else if (is("--device", "--device")) {
+            std::string v;
+            if (!value(v)) return 114;
+            a.device = std::atoi(v.c_str());
+        } else if (is("--bin", "--bin")) {
+            if (!value(a.binPrefix)) return 114;
+        } else if (s.size() > 1 && s[0] == '-') {
+            extras.push_back(s);
+        } else {
+            pos.push_back(s);
+        }
+    }
+    if (pos.size() > 2) extras.insert(extras.end(), pos.begin() + 2, pos.end());
+    if (!extras.empty()) {
+        std::cerr << "The following arguments were not expected:";
+        for (auto& e : extras) std::cerr << " " << e;
+        std::cerr << "\nRun with --help for more information.\n";
+        return 109;  // CLI11 ExtrasError
+    }
+    if (pos.size() >= 1) a.pathToDatabase = pos[0];
+    if (pos.size() >= 2) a.pathToOutputFile = pos[1];
+    auto must_exist = [](const std::string& opt, const std::string& p) {
+        if (!p.empty() && !is_file(p)) {
+            std::cerr << opt << ": File does not exist: " << p << "\nRun with --help for more information.\n";
+            return false;
+        }
+        return true;
+    };
+    if (pos.empty()) {
+        std::cerr << "path_to_input_db is required\nRun with --help for more information.\n";
+        return 106;  // CLI11 RequiredError
+    }
+    if (!must_exist("path_to_input_db", a.pathToDatabase)) return 105;  // CLI11 ValidationError
+    if (pos.size() < 2) {
+        std::cerr << "path_to_output_file is required\nRun with --help for more information.\n";
+        return 106;
+    }
+    if (!must_exist("--query_db", a.pathToQryDatabase)) return 105;
+    if (!must_exist("--query_subset", a.pathToQrySubsetFile)) return 105;
+    return -1;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+template <typename DS>
+int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
+    auto t0 = std::chrono::steady_clock::now();
+    try {
+        pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, app.device, app.refCompat);
+        impl.run();
+        std::printf("AJI (MI355X)        : %10.2f ms  (|E| = %lld; work lists %.2f ms, rows %.2f ms)\n",
+                    ms_since(t0), (long long)impl.nEvents(), impl.msBuild(), impl.msRows());
+        if (app.pathToOutputFile.empty()) return 0;
+        auto t1 = std::chrono::steady_clock::now();
+        std::printf("Writing output with %lld query genomes and %lld target genomes. \n",
+                    (long long)ds.qrySetSize(), (long long)ds.tgtSetSize());
+        auto M = dense_matrix(ds, impl.getJAC(), impl.getAJI(), isSubset);
+        if (write_csv(app.pathToOutputFile, ds.refQuerySet(), ds.refTargetSet(), M, app.outFieldSeparator)) {
+            std::cerr << "Error in writing " << app.pathToOutputFile << std::endl;
+            return 1;
+        }
+        if (!app.binPrefix.empty())
+            write_bin(app.binPrefix, impl.getJAC(), impl.getAJI(), M, ds.qrySetSize(), ds.tgtSetSize());
+        std::printf("Output              : %10.2f ms\n", ms_since(t1));
+    } catch (const pfaai::HipError& e) {
+        std::cerr << "MI355X engine error " << e.code << ": " << e.what() << std::endl;
+        return e.code;
+    }
+    return 0;
+}
+
+int parallel_fastaai(const AppParams& app) {  // main.cpp:177-202
+    DBMetaData meta;
+    LoadedArrays arr;
+    std::string err;
+    auto t0 = std::chrono::steady_clock::now();
+    if (int rc = load_single(app.pathToDatabase, meta, arr, err)) {
+        std::cerr << err << std::endl;
+        return rc;
+    }
+    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    AllData ds(std::move(meta), std::move(arr));
+    return run_and_print(ds, PFAAI_MODE_ALL, app, true);
+}
+
+int validate_subset(const AppParams& app, const DBMetaData& meta) {  // main.cpp:204-232
+    std::unordered_set<std::string> db(meta.genomeSet.begin(), meta.genomeSet.end());
+    std::vector<std::string> missing;
+    for (auto& g : app.qryGenomeSet)
+        if (!db.count(g)) missing.push_back(g);
+    if (!missing.empty()) {
+        std::cout << "--------------------ERROR-----------------------------\n"
+                  << " In the query subset file, the following genomes are \n"
+                  << " missing from the database : \n";
+        for (std::size_t i = 0; i < missing.size(); ++i) std::cout << (i ? "\n    " : "    ") << missing[i];
+        std::cout << "\n\n Please remove them and before running Fast AAI. \n"
+                  << "------------------------------------------------------\n";
+        return 3;
+    }
+    return 0;
+}
+
+int parallel_subset_fastaai(const AppParams& app) {  // main.cpp:234-266
+    DBMetaData meta;
+    LoadedArrays arr;
+    std::string err;
+    auto t0 = std::chrono::steady_clock::now();
+    if (int rc = load_single(app.pathToDatabase, meta, arr, err)) {
+        std::cerr << err << std::endl;
+        return rc;
+    }
+    if (validate_subset(app, meta)) return 3;
+    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    QSubData ds(std::move(meta), std::move(arr), app.qryGenomeSet);
+    return run_and_print(ds, PFAAI_MODE_QSUB, app, true);
+}
+
+int validate_qry2tgt(const DBMetaData& meta) {  // main.cpp:268-300
+    std::unordered_set<std::string> db(meta.genomeSet.begin(), meta.genomeSet.end());
+    std::vector<std::string> common;
+    for (auto& g : meta.qyGenomeSet)
+        if (db.count(g)) common.push_back(g);
+    if (!common.empty()) {
+        std::cout << "---------------------ERROR------------------------------\n"
+                  << "  Query database should have no intersecting genes with \n"
+                  << "  the main data base.\n\n"
+                  << "  In the query data base, the following genomes are \n"
+                  << "  overlapping with the target database:\n";
+        for (std::size_t i = 0; i < common.size(); ++i) std::cout << (i ? "\n    " : "    ") << common[i];
+        std::cout << "\n\n  Please remove them before running Fast AAI.\n"
+                  << "--------------------------------------------------------\n";
+        return 3;
+    }
+    return 0;
+}
+
+int parallel_qry2tgt_fastaai(const AppParams& app) {  // main.cpp:302-335
+    DBMetaData meta;
+    LoadedArrays arr;
+    std::string err;
+    auto t0 = std::chrono::steady_clock::now();
+    if (int rc = load_qt(app.pathToDatabase, app.pathToQryDatabase, meta, arr, err)) {
+        std::cerr << err << std::endl;
+        return rc;
+    }
+    if (validate_qry2tgt(meta)) return 3;
+    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    QTData ds(std::move(meta), std::move(arr));
+    return run_and_print(ds, PFAAI_MODE_QT, app, false);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {  // main.cpp:337-356
+    AppParams app;
+    int rc = parse(argc, argv, app);
+    if (rc >= 0) return rc;
+    app.print();
+    if (app.pathToQryDatabase.empty() || app.pathToQryDatabase == app.pathToDatabase) {
+        if (app.pathToQrySubsetFile.empty()) return parallel_fastaai(app);
+        app.load_query_genomes();
+        return parallel_subset_fastaai(app);
+    }
+    return parallel_qry2tgt_fastaai(app);
+}

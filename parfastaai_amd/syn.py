@@ -40,7 +40,7 @@ def _load():
         L = ctypes.CDLL(LIB)
         vp = ctypes.c_void_p
         L.syn_counts.restype, L.syn_counts.argtypes = ctypes.c_int64, [vp, vp]
-        L.syn_fill.restype, L.syn_fill.argtypes = ctypes.c_int, [vp, vp, vp, vp, vp, vp]
+        L.syn_fill.restype, L.syn_fill.argtypes = ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]
         L.syn_genome_set.restype, L.syn_genome_set.argtypes = ctypes.c_int32, [vp, ctypes.c_int32, ctypes.c_int32, vp]
         _lib = L
     return _lib
@@ -60,8 +60,10 @@ def _p(a):
 
 def generate(n_genomes, n_prot=100, **kw) -> dict:
     """-> dict(Lp int64[160001], F_prot, F_genome int32[|F|], T int32[P, G],
-    genome_set, protein_set) ordered exactly as the reference's loader
-    would produce them from the equivalent SQLite DB."""
+    G_off int64[G*P+1], G_tet int32[|F|], genome_set, protein_set): F ordered
+    exactly as the reference's loader would produce it from the equivalent
+    SQLite DB, G = the genome-major `<p>_genomes` sets ((genome, protein)-major
+    CSR)."""
     prm = params(n_genomes, n_prot, **kw)
     L = _load()
     T = np.zeros((n_prot, n_genomes), dtype=np.int32)
@@ -69,13 +71,13 @@ def generate(n_genomes, n_prot=100, **kw) -> dict:
     Lp = np.zeros(NTETRAMERS + 1, dtype=np.int64)
     Fp = np.empty(nf, dtype=np.int32)
     Fg = np.empty(nf, dtype=np.int32)
-    work = np.empty(max(nf, 1), dtype=np.int32)
-    rc = L.syn_fill(ctypes.byref(prm), _p(T), _p(Lp), _p(Fp), _p(Fg), _p(work))
-    del work
+    G_off = np.zeros(n_genomes * n_prot + 1, dtype=np.int64)
+    G_tet = np.empty(max(nf, 1), dtype=np.int32)
+    rc = L.syn_fill(ctypes.byref(prm), _p(T), _p(Lp), _p(Fp), _p(Fg), _p(G_off), _p(G_tet))
     if rc:
         raise RuntimeError("syn_fill failed")
-    return dict(Lp=Lp, F_prot=Fp, F_genome=Fg, T=T, genome_set=genome_names(n_genomes),
-                protein_set=protein_names(n_prot), params=prm)
+    return dict(Lp=Lp, F_prot=Fp, F_genome=Fg, T=T, G_off=G_off, G_tet=G_tet[:nf],
+                genome_set=genome_names(n_genomes), protein_set=protein_names(n_prot), params=prm)
 
 
 def genome_names(n, prefix="syn"):

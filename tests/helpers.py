@@ -51,9 +51,10 @@ def jac_fixture(name):
     return fm.read_jac(gpath(name + "_jac.bin")), fm.read_vec_f64(gpath(name + "_aji.bin"))
 
 
-def syn_case(name):
+def syn_case(name, genome_major=False):
     """(DataStruct, reference CSV matrix) for a tests/golden/ref_<name>.csv.gz case
-    (see tests/golden/make_ref_vectors.py)."""
+    (see tests/golden/make_ref_vectors.py).  genome_major attaches the
+    `<p>_genomes` view (G) so the engine takes its sort-free work-list path."""
     import make_ref_vectors as mk  # noqa
     from parfastaai_amd import syn
     kind, kw = mk.CASES[name]
@@ -68,11 +69,14 @@ def syn_case(name):
         ds = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"],
                                         [g["genome_set"][i] for i in query])
     else:
-        ds = qt_syn(kw)
+        ds = qt_syn(kw, genome_major)
+        return ds, M
+    if genome_major:
+        ds.with_genome_major(g["G_off"], g["G_tet"])
     return ds, M
 
 
-def qt_syn(kw):
+def qt_syn(kw, genome_major=False):
     """QT arrays for two SYN DBs exactly as the reference's QT loader joins
     them (scp_db.hpp:450-528): per (t, p) block target genomes then query
     genomes offset by nT, only tetramers present in both; T side by side."""
@@ -94,7 +98,11 @@ def qt_syn(kw):
     Lc = np.bincount(t, minlength=160000)
     T = np.concatenate([gt["T"], gq["T"]], axis=1)
     F = np.stack([p, g], axis=1).astype(np.int32)
-    return ParFAAIQryTgtData(Lc, F, T, gt["genome_set"], syn.genome_names(nQ, "qry"), gt["protein_set"][:P])
+    ds = ParFAAIQryTgtData(Lc, F, T, gt["genome_set"], syn.genome_names(nQ, "qry"), gt["protein_set"][:P])
+    if genome_major:  # both DBs' <p>_genomes lists; tetramers absent from F are ignored
+        G_off = np.concatenate([gt["G_off"], gq["G_off"][1:] + gt["G_off"][-1]])
+        ds.with_genome_major(G_off, np.concatenate([gt["G_tet"], gq["G_tet"]]))
+    return ds
 
 
 def _blocks(g):

@@ -28,12 +28,12 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert _capi.load_library().pfaai_version() == 1
+    assert _capi.load_library().pfaai_version() == 2
 
 
 def test_problem_struct_layout():
-    # pfaai_problem: 6 x int32, int64, 7 pointers
-    assert ctypes.sizeof(_capi.Problem) == 6 * 4 + 8 + 7 * 8
+    # pfaai_problem: 6 x int32, int64, 9 pointers
+    assert ctypes.sizeof(_capi.Problem) == 6 * 4 + 8 + 9 * 8
 
 
 def test_no_silent_cpu_fallback_without_gpu():

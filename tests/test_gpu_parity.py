@@ -66,7 +66,7 @@ def test_hip_qt_correct_vs_oracle(engine):
 
 
 @pytest.mark.parametrize("prefix", ["xdb_subset1", "xdb_subset2"])
-def test_hip_counts_equal_sorted_e_runs(engine, prefix):
+def test_hip_counts_equal_sorted_e_runs(engine, prefix):  # noqa: D103
     """Integer intersection counts c(p,a,b) == run-lengths of the reference's sorted E."""
     ds = all_ds(prefix)
     impl = ParFAAIImpl(ds, engine=engine)
@@ -92,19 +92,26 @@ def test_hip_qt_counts_equal_sorted_e_runs(engine):
         assert np.array_equal(C, ref)
 
 
+@pytest.mark.parametrize("gm", [False, True], ids=["F-only", "genome-major"])
 @pytest.mark.parametrize("name", ["all48", "all32_sparse", "qsub40", "qt12"])
-def test_hip_vs_reference_binary_outputs(engine, name):
-    ds, M_ref = syn_case(name)
+def test_hip_vs_reference_binary_outputs(engine, name, gm):
+    ds, M_ref = syn_case(name, genome_major=gm)
     compat = name.startswith("qt")
     impl = ParFAAIImpl(ds, ref_compat=compat, engine=engine)
     impl.run()
     assert np.array_equal(impl.output_matrix(), M_ref)
 
 
-@pytest.mark.parametrize("n,P,k", [(300, 100, 20), (130, 40, 7), (2, 3, 1)])
-def test_hip_vs_oracle_synthetic(engine, n, P, k):
-    g = syn.generate(n, P, clade_size=k)
+def _syn_all(n, P, gm, **kw):
+    g = syn.generate(n, P, **kw)
     ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"])
+    return ds.with_genome_major(g["G_off"], g["G_tet"]) if gm else ds
+
+
+@pytest.mark.parametrize("gm", [False, True], ids=["F-only", "genome-major"])
+@pytest.mark.parametrize("n,P,k", [(300, 100, 20), (130, 40, 7), (2, 3, 1)])
+def test_hip_vs_oracle_synthetic(engine, n, P, k, gm):
+    ds = _syn_all(n, P, gm, clade_size=k)
     impl = ParFAAIImpl(ds, engine=engine)
     impl.run()
     r = O.Problem(ds.problem()).ref_run()
@@ -114,10 +121,13 @@ def test_hip_vs_oracle_synthetic(engine, n, P, k):
     assert np.array_equal(impl.getAJI(), r["AJI"])
 
 
-def test_hip_unsorted_query_list_correct_mode(engine):
+@pytest.mark.parametrize("gm", [False, True], ids=["F-only", "genome-major"])
+def test_hip_unsorted_query_list_correct_mode(engine, gm):
     g = syn.generate(60, 12, clade_size=6)
     q = [g["genome_set"][i] for i in (50, 3, 17, 40, 8)]
     ds = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"], q)
+    if gm:
+        ds.with_genome_major(g["G_off"], g["G_tet"])
     impl = ParFAAIImpl(ds, engine=engine)
     impl.run()
     r = O.Problem(ds.problem(), compat=False).ref_run()
@@ -157,10 +167,10 @@ def test_hip_zero_overlap_pair(engine, compat):
     assert (jac["N"][k] == 1) == compat
 
 
-def test_hip_row_sharding_matches_full(engine):
+@pytest.mark.parametrize("gm", [False, True], ids=["F-only", "genome-major"])
+def test_hip_row_sharding_matches_full(engine, gm):
     """Rows split over 'ranks' (pfaai_run on row ranges) == one full run."""
-    g = syn.generate(257, 30, clade_size=9)
-    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"])
+    ds = _syn_all(257, 30, gm, clade_size=9)
     impl = ParFAAIImpl(ds, engine=engine)
     impl.run()
     full = impl.getAJI()
@@ -180,11 +190,11 @@ def test_hip_row_sharding_matches_full(engine):
     assert np.array_equal(out, full)
 
 
-def test_hip_c2_scale_properties(engine):
+@pytest.mark.parametrize("gm", [False, True], ids=["F-only", "genome-major"])
+def test_hip_c2_scale_properties(engine, gm):
     """Full C2-size run (SYN 2000 x 100): |E| equals the oracle's count,
     sampled rows equal the oracle exactly, AJI in [0, 1]."""
-    g = syn.generate(2000, 100)
-    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"])
+    ds = _syn_all(2000, 100, gm)
     impl = ParFAAIImpl(ds, engine=engine)
     impl.run()
     pr = O.Problem(ds.problem())

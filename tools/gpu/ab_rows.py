@@ -1,0 +1,51 @@
+"""Interleaved A/B of k_rows variants in one process (SYN all-vs-all).
+
+    python tools/gpu/ab_rows.py --genomes 10000 --rounds 5 --variants OCC=2 OCC=1
+Each variant is an env setting read by pfaai_run (PFAAI_ROWS_OCC ...).
+Prints per-variant median/min of build and row-kernel device times.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+from parfastaai_amd import _capi, syn  # noqa: E402
+from parfastaai_amd.datastruct import ParFAAIData  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--genomes", type=int, default=10000)
+ap.add_argument("--prot", type=int, default=100)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--f-only", action="store_true")
+ap.add_argument("--variants", nargs="+", default=["PFAAI_ROWS_OCC=2", "PFAAI_ROWS_OCC=1"])
+a = ap.parse_args()
+g = syn.generate(a.genomes, a.prot)
+ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+if not a.f_only:
+    ds.with_genome_major(g["G_off"], g["G_tet"])
+eng = _capi.Engine(0)
+eng.load(**ds.problem())
+n_rows, n_pairs = eng.shape()
+d = eng.alloc(n_pairs * 8)
+res = {v: ([], []) for v in a.variants}
+ref = None
+for r in range(a.rounds + 1):
+    for v in a.variants:
+        k, val = v.split("=")
+        os.environ[k] = val
+        eng.timing(reset=True)
+        eng.run(0, n_rows, 0, d)
+        n, b, rr = eng.timing(reset=True)
+        out = eng.d2h(d, n_pairs, np.float64)
+        if ref is None:
+            ref = out
+        assert np.array_equal(out, ref), f"variant {v} differs"
+        if r:
+            res[v][0].append(b); res[v][1].append(rr)
+for v, (b, rr) in res.items():
+    print(f"{v:28s} build med {np.median(b):8.3f} min {np.min(b):8.3f} | rows med {np.median(rr):8.3f} min {np.min(rr):8.3f} ms")
+eng.free(d)

@@ -139,19 +139,21 @@ int64_t syn_counts(const syn_params* p, int32_t* T) {
 }
 
 /*
- * Pass 2: given T (from pass 1), fill Lp[NTET+1], F_prot/F_genome[|F|]
- * ordered by (tetramer, protein, genome).  work: int32 scratch of |F|.
+ * Pass 2: given T (from pass 1), fill
+ *   G_off[n_genomes * n_prot + 1], G_tet[|F|]: the genome-major sets (the
+ *       `<p>_genomes` blobs), (genome, protein)-major CSR;
+ *   Lp[NTET + 1], F_prot / F_genome[|F|]: F ordered by (tetramer, protein,
+ *       genome) (the `<p>_tetras` rows, as the reference's loader orders them).
  */
-int syn_fill(const syn_params* p, const int32_t* T, int64_t* Lp, int32_t* Fp, int32_t* Fg, int32_t* work) {
+int syn_fill(const syn_params* p, const int32_t* T, int64_t* Lp, int32_t* Fp, int32_t* Fg, int64_t* G_off,
+             int32_t* G_tet) {
     const int32_t G = p->n_genomes, P = p->n_prot, C = n_clades_of(p);
-    /* CSR of sets in (prot, genome) order */
-    int64_t* off = (int64_t*)malloc(sizeof(int64_t) * ((int64_t)P + 1));
-    off[0] = 0;
-    for (int32_t prot = 0; prot < P; prot++) {
-        int64_t s = 0;
-        for (int32_t g = 0; g < G; g++) s += T[(int64_t)prot * G + g];
-        off[prot + 1] = off[prot] + s;
-    }
+    G_off[0] = 0;
+    for (int32_t g = 0; g < G; g++)
+        for (int32_t prot = 0; prot < P; prot++) {
+            const int64_t k = (int64_t)g * P + prot;
+            G_off[k + 1] = G_off[k] + T[(int64_t)prot * G + g];
+        }
     int bad = 0;
 #pragma omp parallel reduction(| : bad)
     {
@@ -159,38 +161,33 @@ int syn_fill(const syn_params* p, const int32_t* T, int64_t* Lp, int32_t* Fp, in
 #pragma omp for schedule(dynamic, 1)
         for (int32_t prot = 0; prot < P; prot++) {
             int32_t cur_clade = -1, na = 0;
-            int64_t o = off[prot];
             for (int32_t g = 0; g < G; g++) {
                 int32_t cl = clade_of(p, g) % C;
                 if (cl != cur_clade) { na = ancestral(p, cl, prot, anc); cur_clade = cl; }
-                int32_t n = genome_set(p, g, prot, anc, na, work + o);
+                int32_t n = genome_set(p, g, prot, anc, na, G_tet + G_off[(int64_t)g * P + prot]);
                 if (n != T[(int64_t)prot * G + g]) bad = 1;
-                o += n;
             }
         }
         free(anc);
     }
-    if (bad) { free(off); return 1; }
-    /* Lc / Lp */
+    if (bad) return 1;
+    const int64_t nf = G_off[(int64_t)G * P];
     memset(Lp, 0, sizeof(int64_t) * (NTET + 1));
-    const int64_t nf = off[P];
-    for (int64_t i = 0; i < nf; i++) Lp[work[i] + 1]++;
+    for (int64_t i = 0; i < nf; i++) Lp[G_tet[i] + 1]++;
     for (int32_t t = 0; t < NTET; t++) Lp[t + 1] += Lp[t];
-    /* stable scatter by tetramer of the (prot, genome)-ordered stream */
+    /* stable scatter by tetramer of the (protein, genome)-ordered stream */
     int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * NTET);
     memcpy(cur, Lp, sizeof(int64_t) * NTET);
-    int64_t i = 0;
     for (int32_t prot = 0; prot < P; prot++)
         for (int32_t g = 0; g < G; g++) {
-            int32_t n = T[(int64_t)prot * G + g];
-            for (int32_t k = 0; k < n; k++, i++) {
-                int64_t pos = cur[work[i]]++;
+            const int64_t o = G_off[(int64_t)g * P + prot], n = G_off[(int64_t)g * P + prot + 1] - o;
+            for (int64_t k = 0; k < n; k++) {
+                int64_t pos = cur[G_tet[o + k]]++;
                 Fp[pos] = prot;
                 Fg[pos] = g;
             }
         }
     free(cur);
-    free(off);
     return 0;
 }
 
