@@ -51,26 +51,6 @@ def log(msg):
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
-def split_rows(n, world):
-    """Contiguous row blocks of the upper triangle with ~equal pairs
-    (row a owns n-1-a pairs)."""
-    before = lambda a: a * n - a * (a + 1) // 2  # pairs in rows < a  # noqa: E731
-    total = n * (n - 1) // 2
-    cuts = [0]
-    for r in range(1, world):
-        target = total * r // world
-        lo, hi = cuts[-1], n
-        while lo < hi:
-            mid = (lo + hi) // 2
-            if before(mid) < target:
-                lo = mid + 1
-            else:
-                hi = mid
-        cuts.append(lo)
-    cuts.append(n)
-    return [(cuts[i], cuts[i + 1]) for i in range(world)]
-
-
 def traffic_from_profiles():
     """HBM bytes per k_rows launch from profiles/pmc_k_rows.json (written by
     tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes)."""
@@ -155,6 +135,7 @@ def main():
 
     from parfastaai_amd import _capi, syn
     from parfastaai_amd.datastruct import ParFAAIData
+    from parfastaai_amd.shard import split_rows
 
     t0 = time.perf_counter()
     g = syn.generate(args.genomes, args.prot)

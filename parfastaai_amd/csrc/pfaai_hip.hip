@@ -231,6 +231,9 @@ void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t
     if (c->occupancy == 2)
         hipLaunchKernelGGL((k_rows<MODE, KW, 2>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 4)
+        hipLaunchKernelGGL((k_rows_pipe<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev,
+                           rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     else if (c->occupancy == 3)
         hipLaunchKernelGGL((k_rows<MODE, KW, 3>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
@@ -546,7 +549,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     if (const char* occ = getenv("PFAAI_ROWS_OCC")) {  // tuning knob (A/B of k_rows variants)
         const int v = atoi(occ);
-        c->occupancy = (v == 1 || v == 3) ? v : 2;
+        c->occupancy = (v == 1 || v == 3 || v == 4) ? v : 2;
     }
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
         HIPCHK(c, hipStreamSynchronize(s));

@@ -737,6 +737,197 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     }
 }
 
+// ---------------------------------------------------------------------------
+// K-S+J, software-pipelined (k_rows_pipe): one barrier per protein.
+// Phase q overlaps three proteins:
+//   (1) the long-range tails of protein q-1 (whole workgroup; extra barrier
+//       only when there are any, i.e. runs longer than 64 after A),
+//   (2) prefetch of protein q+1's work list into registers,
+//   (3) the scatter of protein q into counter buffer q&1,
+//   (4) the normalisation of protein q-1 from buffer (q-1)&1 (S, N updated
+//       in ascending protein order, counters cleared),
+//   (5) the prefetched list stored into the other LDS stage buffer.
+// so the member-load latency of q hides behind the normalisation of q-1 and
+// the list load of q+1 behind both.
+// ---------------------------------------------------------------------------
+constexpr int kLongMax = 256;
+
+template <int MODE>
+__device__ __forceinline__ uint32_t scatter_pipe(const Dev& d, int32_t a, const uint2* stage,
+                                                 const uint2* __restrict__ recs, uint64_t rb, int n, uint32_t* acc,
+                                                 uint2* longq, int* nlong, int32_t cc0, int32_t cc1) {
+    const int tid = threadIdx.x;
+    const int grp = tid / kGroup, gl = tid % kGroup;
+    uint32_t ev = 0;
+    for (int j = grp; j < n; j += kNumGroups * 4) {
+        uint32_t lo[4], hi[4];
+        int32_t b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = j + u * kNumGroups;
+            const uint2 r = k < n ? (k < kRowThreads ? stage[k] : recs[rb + k]) : make_uint2(0u, 0u);
+            lo[u] = r.x;
+            hi[u] = r.y;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = lo[u] + gl < hi[u] ? d.Fg[lo[u] + gl] : -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) scatter_one<MODE>(d, a, b[u], acc, cc0, cc1, ev);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t cut = hi[u] - lo[u] > kLongCut ? lo[u] + kLongCut : hi[u];
+            if (cut < hi[u]) {  // hand the tail to the whole workgroup (next phase)
+                int slot = 0;
+                if (gl == 0) slot = atomicAdd(nlong, 1);
+                slot = __shfl(slot, 0, kGroup);
+                if (slot < kLongMax) {
+                    if (gl == 0) longq[slot] = make_uint2(cut, hi[u]);
+                } else {
+                    cut = hi[u];  // queue full: the group walks it
+                }
+            }
+            for (uint32_t m = lo[u] + kGroup + gl; m < cut; m += kGroup)
+                scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
+        }
+    }
+    return ev;
+}
+
+template <int KW>
+__device__ __forceinline__ void normalize_protein(const Dev& d, int p, int32_t tca, bool compat, uint32_t* acc,
+                                                  int32_t ncw, int32_t cc0, double* S, uint32_t* N) {
+    const int tid = threadIdx.x;
+    const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
+    const int32_t ta = Tp[tca];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const int32_t w = tid + k * kRowThreads;
+        if (w < ncw) {
+            const uint32_t v = acc[w];
+            if (v) {
+                acc[w] = 0u;
+                const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+                const int32_t b0 = cc0 + 2 * w;
+                if (c0) {
+                    const int32_t tb = Tp[compat ? d.tcol_col[b0] : b0];
+                    S[2 * k] += (double)c0 / (double)(ta + tb - c0);
+                    N[k] += 1u;
+                }
+                if (c1) {
+                    const int32_t tb = Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
+                    S[2 * k + 1] += (double)c1 / (double)(ta + tb - c1);
+                    N[k] += 1u << 16;
+                }
+            }
+        }
+    }
+}
+
+template <int MODE, int KW>
+__global__ __launch_bounds__(kRowThreads, 8) void k_rows_pipe(
+    Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
+    const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
+    const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out,
+    int32_t* __restrict__ n_out, unsigned long long* __restrict__ n_events) {
+    extern __shared__ uint32_t acc2[];  // two counter rows of KW * 1024 words
+    __shared__ uint2 stage[2][kRowThreads];
+    __shared__ uint2 longq[2][kLongMax];
+    __shared__ int nlong[2];
+    const int tid = threadIdx.x;
+    const int64_t rl = blockIdx.x;
+    const int32_t a = d.row_genome[row_begin + rl];
+    int32_t clo, chi;
+    row_cols<MODE>(d, a, clo, chi);
+    const int32_t cc0 = clo + (int32_t)blockIdx.y * chunk_cols;
+    const int32_t cc1 = min(chi, cc0 + chunk_cols);
+    if (cc0 >= cc1) return;  // uniform
+    const int32_t ncw = (cc1 - cc0 + 1) >> 1;
+    constexpr int32_t kStride = KW * kRowThreads;
+    const bool compat = flags & 1u;
+    const int P = d.n_prot;
+    const unsigned long long* rp = rowptr + rl * P;
+
+    for (int w = tid; w < ncw; w += kRowThreads) { acc2[w] = 0u; acc2[kStride + w] = 0u; }
+    if (tid < 2) nlong[tid] = 0;
+    double S[2 * KW];
+    uint32_t N[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
+    const int32_t tca = compat ? d.tcol_row[a] : a;
+    uint32_t ev = 0;
+
+    uint64_t rb_cur = rp[0];
+    int n_cur = (int)(rp[1] - rb_cur);
+    if (tid < n_cur) stage[0][tid] = recs[rb_cur + tid];
+    int n_prev = 0;
+    __syncthreads();
+
+    for (int q = 0; q <= P; ++q) {
+        const int bq = q & 1;
+        uint32_t* acc_q = acc2 + bq * kStride;
+        uint32_t* acc_p = acc2 + (bq ^ 1) * kStride;
+        // (1) long tails of protein q-1
+        if (q >= 1) {
+            const int nl = min(nlong[bq ^ 1], kLongMax);
+            if (nl > 0) {
+                for (int i = 0; i < nl; ++i) {
+                    const uint2 r = longq[bq ^ 1][i];
+                    for (uint32_t m = r.x + tid; m < r.y; m += kRowThreads)
+                        scatter_one<MODE>(d, a, d.Fg[m], acc_p, cc0, cc1, ev);
+                }
+                __syncthreads();
+            }
+        }
+        // (2) prefetch protein q+1's list
+        uint64_t rb_next = 0;
+        int n_next = 0;
+        uint2 pre = make_uint2(0u, 0u);
+        if (q + 1 < P) {
+            rb_next = rp[q + 1];
+            n_next = (int)(rp[q + 2] - rb_next);
+            if (tid < n_next) pre = recs[rb_next + tid];
+        }
+        // (3) scatter protein q
+        if (q < P && n_cur > 0)
+            ev += scatter_pipe<MODE>(d, a, stage[bq], recs, rb_cur, n_cur, acc_q, longq[bq], &nlong[bq], cc0, cc1);
+        // (4) normalise protein q-1
+        if (q >= 1 && n_prev > 0) normalize_protein<KW>(d, q - 1, tca, compat, acc_p, ncw, cc0, S, N);
+        // (5) stage protein q+1
+        if (tid < n_next && tid < kRowThreads) stage[bq ^ 1][tid] = pre;
+        if (tid == 0) nlong[bq ^ 1] = 0;
+        n_prev = q < P ? n_cur : 0;
+        rb_cur = rb_next;
+        n_cur = n_next;
+        __syncthreads();
+    }
+
+    ev = wave_sum_u32(ev);
+    if ((tid & 63) == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const int32_t w = tid + k * kRowThreads;
+        if (w >= ncw) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int32_t b = cc0 + 2 * w + h;
+            if (b >= cc1 || !col_valid<MODE>(d, a, b)) continue;
+            const int64_t idx = pair_index<MODE>(d, a, b, compat);
+            double s = S[2 * k + h];
+            int32_t n = (int32_t)((N[k] >> (16 * h)) & 0xFFFFu);
+            if (n == 0 && compat) {
+                const unsigned long long key = *first_key;
+                const int32_t p0 = key == ~0ull ? 0 : (int32_t)(key & ((1ull << 21) - 1));
+                const int32_t* Tp = d.T + (int64_t)p0 * d.t_cols;
+                s = 0.0 + 1.0 / (double)(Tp[tca] + Tp[d.tcol_col[b]] - 1);
+                n = 1;
+            }
+            if (aji) aji[idx] = n ? s / (double)n : 0.0;
+            if (s_out) s_out[idx] = s;
+            if (n_out) n_out[idx] = n;
+        }
+    }
+}
+
 // Debug: dump the per-protein counts of one row (integer parity vs E).
 template <int MODE>
 __global__ __launch_bounds__(kRowThreads) void k_row_counts(

@@ -38,6 +38,8 @@ struct AppParams {  // main.cpp:56-131
     std::vector<std::string> qryGenomeSet;
     bool refCompat = false;
     int device = 0;
+    std::string dumpPrefix;    // --dump-arrays: write the loader's Lc/F/T (cereal) and exit (no GPU)
+    std::string formatSelftest;  // --format-selftest FILE: print fmt-formatted doubles (hex input)
 
     void print() const {
         std::vector<std::string> args = {" Input Database  : " + pathToDatabase + " ",
@@ -116,6 +118,11 @@ int parse(int argc, char** argv, AppParams& a) {
             a.device = std::atoi(v.c_str());
         } else if (is("--bin", "--bin")) {
             if (!value(a.binPrefix)) return 114;
+        } else if (is("--dump-arrays", "--dump-arrays")) {
+            if (!value(a.dumpPrefix)) return 114;
+        } else if (is("--format-selftest", "--format-selftest")) {
+            if (!value(a.formatSelftest)) return 114;
+            return -2;
         } else if (s.size() > 1 && s[0] == '-') {
             extras.push_back(s);
         } else {
@@ -156,6 +163,29 @@ double ms_since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+// --dump-arrays: the loader's arrays in the reference's fixture format
+// (vector<int> Lc, vector<DPair<int,int>> F, DMatrix<int> T), no GPU.
+int dump_arrays(const std::string& prefix, const LoadedArrays& arr) {
+    auto put = [](FILE* f, const void* p, std::size_t n) { return std::fwrite(p, 1, n, f) == n; };
+    bool ok = true;
+    if (FILE* f = std::fopen((prefix + "_lc_array.bin").c_str(), "wb")) {
+        uint64_t n = arr.Lc.size();
+        ok &= put(f, &n, 8) && put(f, arr.Lc.data(), 4 * n);
+        std::fclose(f);
+    } else ok = false;
+    if (FILE* f = std::fopen((prefix + "_f_array.bin").c_str(), "wb")) {
+        uint64_t n = arr.F.size();
+        ok &= put(f, &n, 8) && put(f, arr.F.data(), 8 * n);
+        std::fclose(f);
+    } else ok = false;
+    if (FILE* f = std::fopen((prefix + "_t_matrix.bin").c_str(), "wb")) {
+        uint64_t h[3] = {arr.T.rows(), arr.T.cols(), arr.T.rows() * arr.T.cols()};
+        ok &= put(f, h, 24) && put(f, arr.T.data.data(), 4 * arr.T.data.size());
+        std::fclose(f);
+    } else ok = false;
+    return ok ? 0 : 1;
+}
+
 template <typename DS>
 int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
     auto t0 = std::chrono::steady_clock::now();
@@ -193,6 +223,7 @@ int parallel_fastaai(const AppParams& app) {  // main.cpp:177-202
         return rc;
     }
     std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
     AllData ds(std::move(meta), std::move(arr));
     return run_and_print(ds, PFAAI_MODE_ALL, app, true);
 }
@@ -225,6 +256,7 @@ int parallel_subset_fastaai(const AppParams& app) {  // main.cpp:234-266
     }
     if (validate_subset(app, meta)) return 3;
     std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
     QSubData ds(std::move(meta), std::move(arr), app.qryGenomeSet);
     return run_and_print(ds, PFAAI_MODE_QSUB, app, true);
 }
@@ -259,6 +291,7 @@ int parallel_qry2tgt_fastaai(const AppParams& app) {  // main.cpp:302-335
     }
     if (validate_qry2tgt(meta)) return 3;
     std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
+    if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
     QTData ds(std::move(meta), std::move(arr));
     return run_and_print(ds, PFAAI_MODE_QT, app, false);
 }
@@ -268,6 +301,17 @@ int parallel_qry2tgt_fastaai(const AppParams& app) {  // main.cpp:302-335
 int main(int argc, char** argv) {  // main.cpp:337-356
     AppParams app;
     int rc = parse(argc, argv, app);
+    if (rc == -2) {  // --format-selftest: one hex double per line -> fmt `{}` text
+        std::ifstream in(app.formatSelftest);
+        std::string s;
+        char buf[48];
+        while (in >> s) {
+            const double v = std::strtod(s.c_str(), nullptr);
+            std::fwrite(buf, 1, fmt_double(v, buf), stdout);
+            std::fputc('\n', stdout);
+        }
+        return 0;
+    }
     if (rc >= 0) return rc;
     app.print();
     if (app.pathToQryDatabase.empty() || app.pathToQryDatabase == app.pathToDatabase) {

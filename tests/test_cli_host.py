@@ -1,0 +1,99 @@
+"""Host side of the drop-in CLI (CPU only): option handling and exit codes,
+the SQLite loader against the reference's fixture arrays, and the fmt-exact
+number format.  The GPU leg is tests/test_gpu_cli.py."""
+import gzip
+import os
+import shutil
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, gpath, text
+from parfastaai_amd import formats as fm
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd")
+
+
+def run(*args, **kw):
+    return subprocess.run([CLI, *args], capture_output=True, text=True, **kw)
+
+
+def unpack(tmp_path, name):
+    out = tmp_path / name
+    with gzip.open(gpath(name)) as fi, open(out, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    return str(out)
+
+
+def test_cli_exit_codes(tmp_path):
+    assert run().returncode == 106                               # RequiredError
+    assert run("/nonexistent.db", "o.csv").returncode == 105     # ValidationError (ExistingFile)
+    db = unpack(tmp_path, "xdb_subset1.db")
+    assert run(db).returncode == 106
+    assert run(db, "o.csv", "-q", "/nonexistent.txt").returncode == 105
+    assert run(db, "o.csv", "--bogus").returncode == 109         # ExtrasError
+    assert run("--help").returncode == 0
+
+
+@pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
+def test_loader_matches_reference_arrays(tmp_path, name):
+    db = unpack(tmp_path, name + ".db")
+    pre = str(tmp_path / "dump")
+    r = run(db, str(tmp_path / "o.csv"), "--dump-arrays", pre)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(fm.read_vec_i32(pre + "_lc_array.bin"), fm.read_vec_i32(gpath(name + "_lc_array.bin")))
+    assert np.array_equal(fm.read_f_array(pre + "_f_array.bin"), fm.read_f_array(gpath(name + "_f_array.bin")))
+    assert np.array_equal(fm.read_matrix_i32(pre + "_t_matrix.bin"), fm.read_matrix_i32(gpath(name + "_t_matrix.bin")))
+
+
+def test_qt_loader_matches_reference_arrays(tmp_path):
+    t = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    pre = str(tmp_path / "dump")
+    r = run(t, str(tmp_path / "o.csv"), "-r", q, "--dump-arrays", pre)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(fm.read_vec_i32(pre + "_lc_array.bin"), fm.read_vec_i32(gpath("xdb_qt_lc_array.bin")))
+    assert np.array_equal(fm.read_f_array(pre + "_f_array.bin"), fm.read_f_array(gpath("xdb_qt_f_array.bin")))
+    assert np.array_equal(fm.read_matrix_i32(pre + "_t_matrix.bin"), fm.read_matrix_i32(gpath("xdb_qt_t_matrix.bin")))
+
+
+def test_bad_query_list_exit_3(tmp_path):
+    # validate_subset (main.cpp:204-232): unknown genome -> error box, rc 3
+    db = unpack(tmp_path, "xdb_subset1.db")
+    ql = unpack(tmp_path, "qsub_test_bad_input.txt")
+    r = run(db, str(tmp_path / "o.csv"), "-q", ql)
+    assert r.returncode == 3 and "missing from the database" in r.stdout
+
+
+def test_overlapping_qt_exit_3(tmp_path):
+    # validate_qry2tgt (main.cpp:268-300): subset1 vs itself-overlapping combo DB
+    t = unpack(tmp_path, "xdb_subset_combo12.db")
+    q = unpack(tmp_path, "xdb_subset1.db")
+    r = run(t, str(tmp_path / "o.csv"), "-r", q)
+    assert r.returncode == 3 and "overlapping" in r.stdout
+
+
+def test_fmt_double_matches_fmt10(tmp_path):
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([
+        rng.random(2000), rng.random(200) * 1e-3, rng.random(50) * 1e-6, rng.random(50) * 1e17,
+        [0.0, 1.0, 0.5, 1e-4, 1e-5, 0.0001234, 1e16, 1e15, 123456789012345.0, 2.0, 1.0009481433436662,
+         9.999999999999999e-05, 5e-324, 1.7976931348623157e308, 0.1, 100.0],
+    ])
+    f = tmp_path / "v.txt"
+    f.write_text("\n".join(float(v).hex() for v in vals) + "\n")
+    r = run("--format-selftest", str(f))
+    assert r.returncode == 0
+    assert r.stdout.splitlines() == [fm.fmt_double(v) for v in vals]
+
+
+def test_fmt_rule_on_fixture_csv():
+    # every cell of the reference's CSV fixtures re-formats to itself
+    for name in ["xanthodb_aji_matrix_wheader.csv", "xdb_subset1_aji_matrix_wheader.csv",
+                 "qsub_test_output_matrix_wheader.csv"]:
+        for line in text(name).splitlines()[1:]:
+            for cell in line.split(",")[1:]:
+                assert fm.fmt_double(float(cell)) == cell

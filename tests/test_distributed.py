@@ -1,0 +1,83 @@
+"""Multi-rank path on CPU (gloo, world_size 2): row-block split + gather.
+
+Each rank computes its own row block (here with the CPU oracle as the
+stand-in for the device, since this runs without a GPU -- the device leg of
+the same split is tests/test_gpu_parity.py::test_hip_row_sharding_matches_full)
+and rank 0 gathers with parfastaai_amd.shard.gather_rows; the gathered vector
+must equal the single-process result exactly.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from parfastaai_amd.shard import split_rows
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, result_q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from parfastaai_amd import syn
+    from parfastaai_amd.datastruct import ParFAAIData
+    from parfastaai_amd.shard import gather_rows, split_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = syn.generate(n, 12, clade_size=5)  # identical on every rank
+    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    pr = O.Problem(ds.problem())
+    blocks = split_rows(n, world)
+    rb, re = blocks[rank]
+    # this rank's rows: oracle dense rows -> JAC order (row a: b = a+1..n-1)
+    S, N, _ = pr.dense_rows(rb, re)
+    aji = [S[a - rb, a + 1:] / N[a - rb, a + 1:] for a in range(rb, re)]
+    local = np.concatenate(aji) if aji else np.zeros(0)
+    counts = [sum(n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
+    t = torch.zeros(max(counts), dtype=torch.float64)
+    t[: len(local)] = torch.from_numpy(local)
+    full = gather_rows(t, counts)
+    if rank == 0:
+        ref = pr.ref_run()["AJI"]
+        result_q.put(bool(np.array_equal(full.numpy(), ref)))
+    dist.destroy_process_group()
+
+
+def test_split_rows_balanced():
+    for n, w in [(10000, 8), (2000, 2), (7, 4), (3, 8)]:
+        blocks = split_rows(n, w)
+        assert blocks[0][0] == 0 and blocks[-1][1] == n
+        assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
+        pairs = [sum(n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
+        if n >= 100 * w:
+            assert max(pairs) - min(pairs) <= n  # within one row
+    assert split_rows(10, 3, all_vs_all=False) == [(0, 3), (3, 6), (6, 10)]
+
+
+def test_gloo_world2_gather_equals_single():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 90, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True

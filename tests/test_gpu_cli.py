@@ -1,0 +1,93 @@
+"""End-to-end drop-in check (GPU): the C++ CLI par_fastaai_amd (SQLite
+loader -> C ABI -> HIP engine -> CSV / cereal bin) reproduces the reference
+CLI's output files byte for byte."""
+import gzip
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import gpath, text
+from parfastaai_amd import formats as fm
+from parfastaai_amd import syn
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd")
+
+
+def unpack(tmp_path, name):
+    out = tmp_path / name
+    with gzip.open(gpath(name)) as fi, open(out, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    return str(out)
+
+
+def run(*args):
+    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return r
+
+
+@pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
+def test_cli_csv_bytes(tmp_path, name):
+    db = unpack(tmp_path, name + ".db")
+    out = tmp_path / "out.csv"
+    run(db, str(out), "--bin", str(tmp_path / "o"))
+    assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
+    J = fm.read_jac(str(tmp_path / "o_jac.bin"))
+    Jr = fm.read_jac(gpath(name + "_jac.bin"))
+    assert np.array_equal(J, Jr)
+    assert np.array_equal(fm.read_vec_f64(str(tmp_path / "o_aji.bin")), fm.read_vec_f64(gpath(name + "_aji.bin")))
+
+
+def test_cli_qt_ref_compat_bins(tmp_path):
+    t = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    run(t, str(tmp_path / "out.csv"), "-r", q, "--ref-compat", "--bin", str(tmp_path / "o"))
+    assert np.array_equal(fm.read_jac(str(tmp_path / "o_jac.bin")), fm.read_jac(gpath("xdb_qt_jac.bin")))
+    assert np.array_equal(fm.read_vec_f64(str(tmp_path / "o_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
+
+
+def test_cli_qt_correct_equals_merged_db_block(tmp_path):
+    """Correct QT semantics = the target x query block of an all-vs-all run on
+    the merged DB (xdb_subset_combo12.db)."""
+    t = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    c = unpack(tmp_path, "xdb_subset_combo12.db")
+    run(t, str(tmp_path / "qt.csv"), "-r", q)
+    run(c, str(tmp_path / "all.csv"))
+    qr, qc, QM = fm.read_csv_matrix(str(tmp_path / "qt.csv"))
+    ar, ac, AM = fm.read_csv_matrix(str(tmp_path / "all.csv"))
+    rows = [ar.index(n) for n in qr]
+    cols = [ac.index(n) for n in qc]
+    assert np.array_equal(QM, AM[np.ix_(rows, cols)])
+
+
+@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12"])
+def test_cli_vs_reference_binary_on_syn(tmp_path, case):
+    import make_ref_vectors as mk
+    kind, kw = mk.CASES[case]
+    kw = dict(kw)
+    out = str(tmp_path / "out.csv")
+    if kind == "all":
+        db = str(tmp_path / "s.db")
+        syn.write_db(db, **kw)
+        run(db, out)
+    elif kind == "qsub":
+        query = kw.pop("query")
+        db = str(tmp_path / "s.db")
+        g = syn.write_db(db, **kw)
+        ql = tmp_path / "q.txt"
+        ql.write_text("\n".join(g["genome_set"][i] for i in query) + "\n")
+        run(db, out, "-q", str(ql))
+    else:
+        nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")
+        tdb, qdb = str(tmp_path / "t.db"), str(tmp_path / "q.db")
+        syn.write_db(tdb, n_genomes=nT, **kw)
+        syn.write_db(qdb, n_genomes=nQ, genome_prefix="qry", genome_seed=syn.DEFAULT_SEED + 1,
+                     n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
+        run(tdb, out, "-r", qdb, "--ref-compat")
+    assert open(out).read() == text(f"ref_{case}.csv")
