@@ -45,19 +45,23 @@ struct pfaai_ctx {
     Dev dev{};
 
     // work space (sized at load for all rows, so runs never allocate)
+    DevBuf cnt_t, off_t;
     DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
     DevBuf out_aji, out_S, out_N, dbg;
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool timed = false;
-    int occupancy = 2;  // k_rows variant: workgroups per CU (PFAAI_ROWS_OCC=1|2)
+    int occupancy = 2;  // k_rows variant (PFAAI_ROWS_OCC=1|2|3|4)
+    int recs_batch = 1;  // k_recs_g chains per lane (PFAAI_RECS_BATCH=1|8)
     // per-run event triples for pfaai_timing (pool reused after each reset)
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;
 };
 
 namespace {
+
+constexpr int kDefaultRowsVariant = 3;  // k_rows: 2 WGs/CU, 4 ranges in flight per group, no tail queue
 
 // scalars buffer layout (u64 each)
 enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
@@ -123,14 +127,19 @@ int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool firs
     auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
     auto* key_c = static_cast<uint32_t*>(c->key_c.p);
     auto* rec_c = static_cast<uint2*>(c->rec_c.p);
-    HIPCHK(c, hipMemsetAsync(sc + SC_NC, 0, sizeof(unsigned long long), s));
+    // compaction offsets: entries per tetramer block, scanned
+    auto* cnt_t = static_cast<uint32_t*>(c->cnt_t.p);
+    auto* off_t = static_cast<unsigned long long*>(c->off_t.p);
+    hipLaunchKernelGGL(k_count_t, dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, rb, re, cnt_t);
+    int rc0 = scan_u32(c, cnt_t, kNTetramers, off_t, s);
+    if (rc0) return rc0;
     if (first_event) HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
     if (first_event)
         hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, rb, re,
-                           key_c, rec_c, sc + SC_NC, sc + SC_FIRST_KEY, err);
+                           key_c, rec_c, off_t, sc + SC_FIRST_KEY, err);
     else
         hipLaunchKernelGGL((k_entries<MODE, false>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, rb, re,
-                           key_c, rec_c, sc + SC_NC, sc + SC_FIRST_KEY, err);
+                           key_c, rec_c, off_t, sc + SC_FIRST_KEY, err);
     if (n == 0) {
         HIPCHK(c, hipMemsetAsync(rowptr, 0, (K + 1) * sizeof(unsigned long long), s));
         HIPCHK(c, hipGetLastError());
@@ -156,8 +165,8 @@ int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool firs
         int rc = scan_u32(c, hist, kRsBins * ntiles, hoff, s);
         if (rc) return rc;
 #define RS(F, L)                                                                                                  \
-    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, ntiles, \
-                       kout, vout, rec_c, recs)
+    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, hist, \
+                       ntiles, kout, vout, rec_c, recs)
         if (first && last) RS(true, true);
         else if (first) RS(true, false);
         else if (last) RS(false, true);
@@ -191,13 +200,20 @@ int build_records_g(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool fi
         HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
         hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
                            (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
-                           sc + SC_NC, sc + SC_FIRST_KEY, err);
+                           static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
     }
     hipLaunchKernelGGL(k_glen, dim3(ceil_div(K, 256)), dim3(256), 0, s, c->dev, rb, K, len);
     int rc = scan_u32(c, len, K, rowptr, s);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_recs_g<MODE>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
-                       static_cast<uint2*>(c->recs.p));
+    if (c->recs_batch == 0 && MODE == 0)
+        hipLaunchKernelGGL((k_recs_g<MODE, 0>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+                           static_cast<uint2*>(c->recs.p));
+    else if (c->recs_batch == 8)
+        hipLaunchKernelGGL((k_recs_g<MODE, 8>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+                           static_cast<uint2*>(c->recs.p));
+    else
+        hipLaunchKernelGGL((k_recs_g<MODE, 1>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+                           static_cast<uint2*>(c->recs.p));
     HIPCHK(c, hipGetLastError());
     return PFAAI_OK;
 }
@@ -230,6 +246,15 @@ void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t
     auto* recs = static_cast<const uint2*>(c->recs.p);
     if (c->occupancy == 2)
         hipLaunchKernelGGL((k_rows<MODE, KW, 2>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 7)
+        hipLaunchKernelGGL((k_rows<MODE, KW, 7>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 6)
+        hipLaunchKernelGGL((k_rows<MODE, KW, 6>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 5)
+        hipLaunchKernelGGL((k_rows4<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), 3 * lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     else if (c->occupancy == 4)
         hipLaunchKernelGGL((k_rows_pipe<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev,
@@ -318,7 +343,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
         release(*b);
@@ -412,6 +437,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     int rc;
     if ((rc = upload(c, c->Lp, p.Lp, PFAAI_NTETRAMERS + 1))) return rc;
     if ((rc = upload(c, c->Fp, p.F_prot, p.n_f))) return rc;
+    if ((rc = ensure(c, c->Fg, (p.n_f + 16) * sizeof(int32_t)))) return rc;  // int4 reads may pass the end
     if ((rc = upload(c, c->Fg, p.F_genome, p.n_f))) return rc;
     if ((rc = upload(c, c->T, p.T, tn))) return rc;
     std::vector<uint8_t> isq(ni, 1);
@@ -490,6 +516,8 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     const int64_t hist_n = kRsBins * ntiles;
     if ((rc = ensure(c, c->rowptr, (K + 1) * sizeof(unsigned long long)))) return rc;
     if ((rc = ensure(c, c->lens, std::max<int64_t>(K, 1) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->off_t, (PFAAI_NTETRAMERS + 1) * sizeof(unsigned long long)))) return rc;
     if ((rc = ensure(c, c->key_c, nmax * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c, c->rec_c, nmax * sizeof(uint2)))) return rc;
     if ((rc = ensure(c, c->key_a, nmax * sizeof(uint32_t)))) return rc;
@@ -499,7 +527,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     if ((rc = ensure(c, c->recs, nmax * sizeof(uint2)))) return rc;
     if ((rc = ensure(c, c->hist, hist_n * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c, c->hoff, (hist_n + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max(hist_n, K), kScanTile)) *
+    if ((rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max({hist_n, K, (int64_t)PFAAI_NTETRAMERS}), kScanTile)) *
                                      sizeof(unsigned long long))))
         return rc;
     HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
@@ -547,10 +575,16 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     if (!aji && !S && !N) return fail(c, PFAAI_ERR_INVALID, "no output");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-    if (const char* occ = getenv("PFAAI_ROWS_OCC")) {  // tuning knob (A/B of k_rows variants)
-        const int v = atoi(occ);
-        c->occupancy = (v == 1 || v == 3 || v == 4) ? v : 2;
+    // tuning knobs for A/B runs (tools/gpu/ab_rows.py); unset = defaults
+    {
+        const char* occ = getenv("PFAAI_ROWS_OCC");
+        const int v = occ ? atoi(occ) : 0;
+        c->occupancy = (v >= 1 && v <= 7) ? v : kDefaultRowsVariant;
+        const char* rbv = getenv("PFAAI_RECS_BATCH");
+        const int r = rbv ? atoi(rbv) : 1;
+        c->recs_batch = (r == 0 || r == 8) ? r : 1;
     }
+    if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
         HIPCHK(c, hipStreamSynchronize(s));
         c->pool_used = 0;

@@ -56,6 +56,23 @@ struct Dev {
     uint2* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run [start, end)
 };
 
+// XCD-aware row order (MI355X_MICROARCH.md: workgroups are dealt round-robin
+// over the 8 XCDs, each with a private 4 MiB L2).  Consecutive rows -- in
+// practice genomes of one clade, which read the same F blocks -- should share
+// an L2: workgroup b (on XCD b % 8) takes row chunk (b/8 / C) * 8 + b % 8,
+// i.e. XCD x walks chunks x, x+8, ... of C consecutive rows.  A bijection on
+// [0, n); the tail that does not fill 8 chunks keeps the identity.  Speed
+// only -- any order is correct.
+constexpr int kXcds = 8;
+constexpr int kXcdChunk = 32;
+
+__device__ __forceinline__ int64_t xcd_row(int64_t b, int64_t n) {
+    const int64_t full = (n / (kXcds * kXcdChunk)) * (kXcds * kXcdChunk);
+    if (b >= full) return b;
+    const int64_t x = b % kXcds, i = b / kXcds;
+    return (i / kXcdChunk) * (kXcds * kXcdChunk) + x * kXcdChunk + (i % kXcdChunk);
+}
+
 // ---------------------------------------------------------------------------
 // mode index maps (ds_impl.hpp:83-96, 251-276, 411-426)
 // ---------------------------------------------------------------------------
@@ -111,10 +128,40 @@ __device__ __forceinline__ int64_t lower_bound_g(const int32_t* Fg, int64_t lo, 
 // lexicographically first E triple (gA, gB, p) over all rows (ref-compat row
 // Z).
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_sum_u32_fwd(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// entries of rows [row_begin, row_end) per tetramer block (compaction offsets)
+__global__ __launch_bounds__(kTetraThreads) void k_count_t(Dev d, int64_t row_begin, int64_t row_end,
+                                                           uint32_t* __restrict__ cnt_t) {
+    __shared__ uint32_t wsum[kTetraThreads / 64];
+    const int tid = threadIdx.x;
+    for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
+        const int64_t s = d.Lp[t], e = d.Lp[t + 1];
+        uint32_t c = 0;
+        for (int64_t i = s + tid; i < e; i += kTetraThreads) {
+            const int32_t row = d.row_of[d.Fg[i]];
+            c += (row >= row_begin && row < row_end) ? 1u : 0u;
+        }
+        c = wave_sum_u32_fwd(c);
+        if ((tid & 63) == 0) wsum[tid >> 6] = c;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (int w = 0; w < kTetraThreads / 64; ++w) tot += wsum[w];
+            cnt_t[t] = tot;
+        }
+        __syncthreads();
+    }
+}
+
 template <int MODE, bool FIRST>
 __global__ __launch_bounds__(kTetraThreads) void k_entries(
     Dev d, int64_t row_begin, int64_t row_end, uint32_t* __restrict__ key_c, uint2* __restrict__ rec_c,
-    unsigned long long* __restrict__ n_c, unsigned long long* __restrict__ first_key, int* __restrict__ err) {
+    const unsigned long long* __restrict__ off_t, unsigned long long* __restrict__ first_key, int* __restrict__ err) {
     __shared__ int32_t runs[kMaxRuns + 1];
     __shared__ int32_t wave_cnt[kTetraThreads / 64];
     __shared__ int32_t n_runs;
@@ -151,7 +198,10 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
             __syncthreads();
         }
         const int nr = min(n_runs, kMaxRuns);
-        if (tid == 0) runs[nr] = (int32_t)(e - s);
+        if (tid == 0) {
+            runs[nr] = (int32_t)(e - s);
+            chunk_base = off_t ? off_t[t] : 0ull;
+        }
         __syncthreads();
 
         for (int64_t base = s; base < e; base += kTetraThreads) {  // uniform trip count
@@ -198,21 +248,21 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
                     }
                 }
             }
-            // order-free compaction: one global atomic per 256 entries
+            // compaction at this tetramer's offset (per-tetramer counts, scanned)
             const unsigned long long m = __ballot(valid);
             if (lane == 0) wave_cnt[wid] = __popcll(m);
             __syncthreads();
-            if (tid == 0) {
-                int tot = 0;
-                for (int w = 0; w < kTetraThreads / 64; ++w) tot += wave_cnt[w];
-                chunk_base = tot ? atomicAdd(n_c, (unsigned long long)tot) : 0ull;
-            }
-            __syncthreads();
-            if (valid) {
+            if (valid && key_c) {
                 unsigned long long off = chunk_base + __popcll(m & lt);
                 for (int w = 0; w < wid; ++w) off += wave_cnt[w];
                 key_c[off] = key;
                 rec_c[off] = rec;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int tot = 0;
+                for (int w = 0; w < kTetraThreads / 64; ++w) tot += wave_cnt[w];
+                chunk_base += tot;
             }
             __syncthreads();
         }
@@ -287,20 +337,21 @@ __global__ void k_glen(Dev d, int64_t row_begin, int64_t n_keys, uint32_t* __res
 // Each thread walks kRecsBatch entries at once: their G, run-table and
 // binary-search loads are issued together (8 independent chains in flight
 // per lane) -- the kernel is bound by dependent-load latency otherwise.
-constexpr int kRecsBatch = 8;
-
-template <int MODE>
+// kRecsBatch = 0: ALL mode only, no search -- the record is the whole run;
+// members B <= A are dropped by the row's column window (cc0 = A + 1).
+template <int MODE, int kRecsBatchT>
 __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_begin,
                                                           const unsigned long long* __restrict__ rowptr,
                                                           uint2* __restrict__ recs) {
     __shared__ long long goff[kMaxRuns + 1];
     const int tid = threadIdx.x;
-    const int64_t rl = blockIdx.x;
+    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
     const int32_t a = d.row_genome[row_begin + rl];
     const int P = d.n_prot;
     const int64_t g0 = (int64_t)a * P;
     for (int p = tid; p <= P; p += kTetraThreads) goff[p] = d.G_off[g0 + p];
     __syncthreads();
+    constexpr int kRecsBatch = kRecsBatchT > 0 ? kRecsBatchT : 1;
     const int64_t k0 = goff[0], k1 = goff[P];
     for (int64_t kb = k0 + tid; kb < k1; kb += (int64_t)kTetraThreads * kRecsBatch) {
         int pr[kRecsBatch];
@@ -328,7 +379,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_beg
             end[u] = run.y;
             live[u] = live[u] && run.y > run.x;
         }
-        if constexpr (MODE != 1) {
+        if constexpr (MODE != 1 && kRecsBatchT > 0) {
             // lockstep lower_bound of A (ALL) or of n_tgt (QT) in each run's sorted genome ids
             const int32_t key = MODE == 0 ? a : d.n_tgt;
             bool any = true;
@@ -356,7 +407,9 @@ __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_beg
             if (k >= k1) continue;
             uint2 rec = make_uint2(0u, 0u);
             if (live[u]) {
-                if constexpr (MODE == 0) {
+                if constexpr (MODE == 0 && kRecsBatchT == 0) {
+                    rec = make_uint2(lo[u], end[u]);  // whole run: B <= A fall outside the column window
+                } else if constexpr (MODE == 0) {
                     if (lo[u] < end[u] && d.Fg[lo[u]] == a) rec = make_uint2(lo[u] + 1u, end[u]);
                 } else if constexpr (MODE == 1) {
                     rec = make_uint2(lo[u], end[u]);
@@ -403,18 +456,39 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restri
 template <bool FIRSTPASS, bool LAST>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, int64_t n, int shift,
-    const unsigned long long* __restrict__ offs, int64_t ntiles, uint32_t* __restrict__ keys_out,
-    uint32_t* __restrict__ vals_out, const uint2* __restrict__ rec_c, uint2* __restrict__ recs_out) {
-    __shared__ unsigned long long base[kRsBins];
-    __shared__ unsigned long long wpos[kRsThreads / 64][kRsBins];
+    const unsigned long long* __restrict__ offs, const uint32_t* __restrict__ hist, int64_t ntiles,
+    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint2* __restrict__ rec_c,
+    uint2* __restrict__ recs_out) {
+    __shared__ uint32_t lkey[kRsTile];
+    __shared__ uint32_t lval[kRsTile];
+    __shared__ uint32_t lstart[kRsBins];  // tile-local start of each digit
+    __shared__ uint32_t base[kRsBins];    // running tile-local position of each digit
+    __shared__ uint32_t wpos[kRsThreads / 64][kRsBins];
     __shared__ uint32_t wcnt[kRsThreads / 64][kRsBins];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    base[tid] = offs[(int64_t)tid * ntiles + blockIdx.x];
+    {  // exclusive scan of this tile's digit counts (hist[digit][tile])
+        const uint32_t c = hist[(int64_t)tid * ntiles + blockIdx.x];
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (lane == 63) wcnt[0][wid] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int w = 0; w < wid; ++w) off += wcnt[0][w];
+        lstart[tid] = off + inc - c;
+        base[tid] = off + inc - c;
+        __syncthreads();
+    }
     const int64_t t0 = (int64_t)blockIdx.x * kRsTile;
+    const int tn = (int)((n - t0) < kRsTile ? (n - t0) : kRsTile);
     for (int r = 0; r < kRsRounds; ++r) {
-        const int64_t j = t0 + r * kRsThreads + tid;
-        const bool valid = j < n;
+        const int li = r * kRsThreads + tid;
+        const bool valid = li < tn;
+        const int64_t j = t0 + li;
         const uint32_t k = valid ? keys_in[j] : 0u;
         const uint32_t v = valid ? (FIRSTPASS ? (uint32_t)j : vals_in[j]) : 0u;
         const uint32_t dig = (k >> shift) & (kRsBins - 1);
@@ -431,8 +505,8 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
         __syncthreads();
         if (valid && rank == 0) wcnt[wid][dig] = __popcll(peers);
         __syncthreads();
-        {  // digit tid: exclusive prefix over waves, advance the running base
-            unsigned long long run = base[tid];
+        {
+            uint32_t run = base[tid];
 #pragma unroll
             for (int w = 0; w < kRsThreads / 64; ++w) {
                 wpos[w][tid] = run;
@@ -442,11 +516,20 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
         }
         __syncthreads();
         if (valid) {
-            const unsigned long long pos = wpos[wid][dig] + rank;
-            keys_out[pos] = k;
-            if (LAST) recs_out[pos] = rec_c[v];
-            else vals_out[pos] = v;
+            const uint32_t lp = wpos[wid][dig] + rank;  // stable tile-local position
+            lkey[lp] = k;
+            lval[lp] = v;
         }
+    }
+    __syncthreads();
+    // write each digit's run of the tile contiguously
+    for (int li = tid; li < tn; li += kRsThreads) {
+        const uint32_t k = lkey[li], v = lval[li];
+        const uint32_t dig = (k >> shift) & (kRsBins - 1);
+        const unsigned long long pos = offs[(int64_t)dig * ntiles + blockIdx.x] + (li - lstart[dig]);
+        keys_out[pos] = k;
+        if (LAST) recs_out[pos] = rec_c[v];
+        else vals_out[pos] = v;
     }
 }
 
@@ -648,12 +731,13 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
     const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
     unsigned long long* __restrict__ n_events) {
-    extern __shared__ uint32_t acc[];
+    extern __shared__ uint32_t acc[];  // KW*1024 counter words (+ OCC 7: a u16 T row of 2*KW*1024)
     __shared__ uint2 rec_lds[kRowThreads];
-    __shared__ uint2 long_lds[kRowThreads];
+    __shared__ uint2 long_lds[OCC == 7 || OCC == 6 ? 1 : kRowThreads];
     __shared__ int n_long;
+    uint16_t* trow = reinterpret_cast<uint16_t*>(acc + KW * kRowThreads);
     const int tid = threadIdx.x;
-    const int64_t rl = blockIdx.x;  // local row
+    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);  // local row
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
     row_cols<MODE>(d, a, clo, chi);
@@ -676,9 +760,24 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     for (int p = 0; p < P; ++p) {
         const uint64_t rb = rowptr[rl * P + p], re = rowptr[rl * P + p + 1];
         if (rb == re) continue;  // uniform: no E triple (p, a, *)
-        ev += scatter_row_protein<MODE, OCC == 1 ? 8 : 4, OCC != 3>(d, a, recs, rb, re, acc, rec_lds, long_lds,
-                                                                    &n_long, cc0, cc1);
+        if (OCC == 7) {  // stage this protein's T row (u16) for the chunk's columns; read after the barrier
+            const int32_t* Tq = d.T + (int64_t)p * d.t_cols;
+            for (int c = tid; c < cc1 - cc0; c += kRowThreads)
+                trow[c] = (uint16_t)Tq[compat ? d.tcol_col[cc0 + c] : cc0 + c];
+        }
+        if (flags & 0x200u) {  // diagnostics: 0x200 skips the scatter
+        } else if (OCC == 6 || OCC == 7) {
+            ev += scatter_row_rle<MODE, 4>(d, a, recs, rb, re, acc, rec_lds, cc0, cc1);
+        } else {
+            ev += scatter_row_protein<MODE, OCC == 1 ? 8 : 4, OCC != 3>(d, a, recs, rb, re, acc, rec_lds, long_lds,
+                                                                        &n_long, cc0, cc1);
+        }
         __syncthreads();
+        if (flags & 0x100u) {  // diagnostics: 0x100 skips the normalisation (counters just cleared)
+            for (int w = tid; w < ncw; w += kRowThreads) acc[w] = 0u;
+            __syncthreads();
+            continue;
+        }
         const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
         const int32_t ta = Tp[tca];
 #pragma unroll
@@ -691,12 +790,13 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     const int32_t b0 = cc0 + 2 * w;
                     if (c0) {
-                        const int32_t tb = Tp[compat ? d.tcol_col[b0] : b0];
+                        const int32_t tb = OCC == 7 ? (int32_t)trow[2 * w] : Tp[compat ? d.tcol_col[b0] : b0];
                         S[2 * k] += (double)c0 / (double)(ta + tb - c0);
                         N[k] += 1u;
                     }
                     if (c1) {
-                        const int32_t tb = Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
+                        const int32_t tb = OCC == 7 ? (int32_t)trow[2 * w + 1]
+                                                    : Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
                         S[2 * k + 1] += (double)c1 / (double)(ta + tb - c1);
                         N[k] += 1u << 16;
                     }
@@ -735,6 +835,72 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
             if (n_out) n_out[idx] = n;
         }
     }
+}
+
+// Scatter with per-lane run-length accumulation (k_rows OCC 6): lane l of a
+// 16-lane group sees member l of each of its ranges; consecutive ranges of
+// one (row, protein) list mostly hold the same genomes at the same offsets
+// (a clade), so the lane keeps (column, count) in registers and only issues
+// an LDS atomic when its column changes -- exact for any input, and it cuts
+// the same-address LDS atomics that dominate clade-structured data.
+template <int MODE>
+__device__ __forceinline__ void rle_push(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0, int32_t cc1,
+                                         int32_t& rcol, uint32_t& rcnt, uint32_t& ev) {
+    if (b < 0) return;
+    if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;
+    if (b < cc0 || b >= cc1) return;
+    ++ev;
+    if (b == rcol) {
+        ++rcnt;
+        return;
+    }
+    if (rcnt) {
+        const uint32_t o = (uint32_t)(rcol - cc0);
+        atomicAdd(&acc[o >> 1], rcnt << ((o & 1u) << 4));
+    }
+    rcol = b;
+    rcnt = 1;
+}
+
+template <int MODE, int kUnroll>
+__device__ __forceinline__ uint32_t scatter_row_rle(const Dev& d, int32_t a, const uint2* __restrict__ recs,
+                                                    uint64_t rb, uint64_t re, uint32_t* acc, uint2* rec_lds,
+                                                    int32_t cc0, int32_t cc1) {
+    const int tid = threadIdx.x;
+    const int grp = tid / kGroup, gl = tid % kGroup;
+    uint32_t ev = 0;
+    int32_t rcol = -1;
+    uint32_t rcnt = 0;
+    for (uint64_t base = rb; base < re; base += kRowThreads) {  // uniform trip count
+        const int n = (int)((re - base) < (uint64_t)kRowThreads ? (re - base) : (uint64_t)kRowThreads);
+        __syncthreads();
+        if (tid < n) rec_lds[tid] = recs[base + tid];
+        __syncthreads();
+        for (int j = grp; j < n; j += kNumGroups * kUnroll) {
+            uint32_t lo[kUnroll], hi[kUnroll];
+            int32_t b[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int k = j + u * kNumGroups;
+                const uint2 r = k < n ? rec_lds[k] : make_uint2(0u, 0u);
+                lo[u] = r.x;
+                hi[u] = r.y;
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) b[u] = lo[u] + gl < hi[u] ? d.Fg[lo[u] + gl] : -1;
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) rle_push<MODE>(d, a, b[u], acc, cc0, cc1, rcol, rcnt, ev);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                for (uint32_t m = lo[u] + kGroup + gl; m < hi[u]; m += kGroup)
+                    scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
+        }
+    }
+    if (rcnt) {
+        const uint32_t o = (uint32_t)(rcol - cc0);
+        atomicAdd(&acc[o >> 1], rcnt << ((o & 1u) << 4));
+    }
+    return ev;
 }
 
 // ---------------------------------------------------------------------------
@@ -834,7 +1000,7 @@ __global__ __launch_bounds__(kRowThreads, 8) void k_rows_pipe(
     __shared__ uint2 longq[2][kLongMax];
     __shared__ int nlong[2];
     const int tid = threadIdx.x;
-    const int64_t rl = blockIdx.x;
+    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
     row_cols<MODE>(d, a, clo, chi);
@@ -924,6 +1090,205 @@ __global__ __launch_bounds__(kRowThreads, 8) void k_rows_pipe(
             if (aji) aji[idx] = n ? s / (double)n : 0.0;
             if (s_out) s_out[idx] = s;
             if (n_out) n_out[idx] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K-S+J v4 (k_rows4): 4-lane groups with 16-byte loads, T row staged in LDS.
+//   * scatter: each group of 4 lanes owns one member range; lane l loads the
+//     int4 at (lo & ~3) + 4l, so one group covers 16 genome ids with one
+//     64-B request (one wave instruction = 16 ranges); members outside
+//     [lo, hi) are masked.  Two ranges per group are in flight.  Ranges
+//     longer than 64 members hand their tail to the whole workgroup.
+//   * per protein the T row of the chunk's columns is staged into LDS as u16
+//     (T < 2^16 is checked at load) while the previous protein is being
+//     normalised, so the normalisation reads no global memory.
+//   * phases: [normalise p-1 | stage list + T row of p] barrier [scatter p]
+//     barrier -- two barriers per protein (three when long tails exist).
+// ---------------------------------------------------------------------------
+constexpr int kG4 = 4;                        // lanes per range
+constexpr int kNumG4 = kRowThreads / kG4;     // 256 ranges per workgroup pass
+constexpr uint32_t kLongCut4 = 64;            // members a group walks before handing off
+
+template <int MODE>
+__device__ __forceinline__ void scatter4(const Dev& d, int32_t a, int4 v, uint32_t pos, uint32_t lo, uint32_t hi,
+                                         uint32_t* acc, int32_t cc0, int32_t cc1, uint32_t& ev) {
+    const int32_t e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t m = pos + e;
+        if (m >= lo && m < hi) scatter_one<MODE>(d, a, e4[e], acc, cc0, cc1, ev);
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t scatter_row4(const Dev& d, int32_t a, const uint2* stage,
+                                                 const uint2* __restrict__ recs, uint64_t rb, int n, uint32_t* acc,
+                                                 uint2* longq, int* nlong, int32_t cc0, int32_t cc1) {
+    const int tid = threadIdx.x;
+    const int grp = tid / kG4, gl = tid % kG4;
+    const int4* F4 = reinterpret_cast<const int4*>(d.Fg);
+    uint32_t ev = 0;
+    for (int j = grp; j < n; j += kNumG4 * 2) {
+        uint32_t lo[2], hi[2], pos[2];
+        int4 v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = j + u * kNumG4;
+            const uint2 r = k < n ? (k < kRowThreads ? stage[k] : recs[rb + k]) : make_uint2(0u, 0u);
+            lo[u] = r.x;
+            hi[u] = r.y;
+            pos[u] = (r.x & ~3u) + 4u * gl;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) v[u] = pos[u] < hi[u] ? F4[pos[u] >> 2] : make_int4(-1, -1, -1, -1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) scatter4<MODE>(d, a, v[u], pos[u], lo[u], hi[u], acc, cc0, cc1, ev);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t base = lo[u] & ~3u;
+            uint32_t cut = hi[u];
+            if (hi[u] > base + kLongCut4) {  // tail to the whole workgroup
+                cut = base + kLongCut4;
+                int slot = 0;
+                if (gl == 0) slot = atomicAdd(nlong, 1);
+                slot = __shfl(slot, 0, kG4);
+                if (slot < kLongMax) {
+                    if (gl == 0) longq[slot] = make_uint2(cut, hi[u]);
+                } else {
+                    cut = hi[u];  // queue full: the group walks it
+                }
+            }
+            for (uint32_t q = base + 16u + 4u * gl; q < cut; q += 16u)
+                scatter4<MODE>(d, a, F4[q >> 2], q, lo[u], cut, acc, cc0, cc1, ev);
+        }
+    }
+    return ev;
+}
+
+template <int MODE, int KW>
+__global__ __launch_bounds__(kRowThreads, 8) void k_rows4(
+    Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
+    const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
+    const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out,
+    int32_t* __restrict__ n_out, unsigned long long* __restrict__ n_events) {
+    extern __shared__ uint32_t smem[];  // acc[KW*1024] words | T rows: 2 x (2*KW*1024) u16
+    __shared__ uint2 stage[kRowThreads];
+    __shared__ uint2 longq[kLongMax];
+    __shared__ int nlong;
+    __shared__ int32_t ta_s[2];
+    constexpr int32_t kWords = KW * kRowThreads;
+    uint32_t* acc = smem;
+    uint16_t* trow = reinterpret_cast<uint16_t*>(smem + kWords);  // [2][2 * kWords]
+    const int tid = threadIdx.x;
+    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
+    const int32_t a = d.row_genome[row_begin + rl];
+    int32_t clo, chi;
+    row_cols<MODE>(d, a, clo, chi);
+    const int32_t cc0 = clo + (int32_t)blockIdx.y * chunk_cols;
+    const int32_t cc1 = min(chi, cc0 + chunk_cols);
+    if (cc0 >= cc1) return;  // uniform
+    const int32_t ncols = cc1 - cc0, ncw = (ncols + 1) >> 1;
+    const bool compat = flags & 1u;
+    const int P = d.n_prot;
+    const unsigned long long* rp = rowptr + rl * P;
+    const int32_t tca = compat ? d.tcol_row[a] : a;
+
+    for (int w = tid; w < ncw; w += kRowThreads) acc[w] = 0u;
+    if (tid == 0) nlong = 0;
+    double S[2 * KW];
+    uint32_t N[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
+    uint32_t ev = 0;
+    int n_prev = 0;
+    uint64_t rb = 0;
+    int n = 0;
+
+    for (int p = 0; p <= P; ++p) {
+        // ---- phase A: normalise p-1, stage p
+        if (p >= 1 && n_prev > 0) {
+            const uint16_t* tr = trow + ((p - 1) & 1) * (2 * kWords);
+            const int32_t ta = ta_s[(p - 1) & 1];
+#pragma unroll
+            for (int k = 0; k < KW; ++k) {
+                const int32_t w = tid + k * kRowThreads;
+                if (w < ncw) {
+                    const uint32_t v = acc[w];
+                    if (v) {
+                        acc[w] = 0u;
+                        const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+                        if (c0) {
+                            S[2 * k] += (double)c0 / (double)(ta + (int32_t)tr[2 * w] - c0);
+                            N[k] += 1u;
+                        }
+                        if (c1) {
+                            S[2 * k + 1] += (double)c1 / (double)(ta + (int32_t)tr[2 * w + 1] - c1);
+                            N[k] += 1u << 16;
+                        }
+                    }
+                }
+            }
+        }
+        if (p < P) {
+            rb = rp[p];
+            n = (int)(rp[p + 1] - rb);
+            if (n > 0) {
+                if (tid < n) stage[tid] = recs[rb + tid];
+                const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
+                uint16_t* tr = trow + (p & 1) * (2 * kWords);
+                for (int c = tid; c < ncols; c += kRowThreads)
+                    tr[c] = (uint16_t)Tp[compat ? d.tcol_col[cc0 + c] : cc0 + c];
+                if (tid == 0) ta_s[p & 1] = Tp[tca];
+            }
+        } else {
+            n = 0;
+        }
+        __syncthreads();
+        // ---- phase B: scatter p
+        if (n > 0 && !(flags & 0x200u)) {
+            ev += scatter_row4<MODE>(d, a, stage, recs, rb, n, acc, longq, &nlong, cc0, cc1);
+            __syncthreads();
+            const int nl = min(nlong, kLongMax);
+            if (nl > 0) {
+                const int4* F4 = reinterpret_cast<const int4*>(d.Fg);
+                for (int i = 0; i < nl; ++i) {
+                    const uint2 r = longq[i];  // r.x is 4-aligned
+                    for (uint32_t q = r.x + 4u * tid; q < r.y; q += 4u * kRowThreads)
+                        scatter4<MODE>(d, a, F4[q >> 2], q, r.x, r.y, acc, cc0, cc1, ev);
+                }
+                __syncthreads();
+                if (tid == 0) nlong = 0;
+            }
+        }
+        __syncthreads();
+        n_prev = n;
+    }
+
+    ev = wave_sum_u32(ev);
+    if ((tid & 63) == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const int32_t w = tid + k * kRowThreads;
+        if (w >= ncw) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int32_t b = cc0 + 2 * w + h;
+            if (b >= cc1 || !col_valid<MODE>(d, a, b)) continue;
+            const int64_t idx = pair_index<MODE>(d, a, b, compat);
+            double s = S[2 * k + h];
+            int32_t nn = (int32_t)((N[k] >> (16 * h)) & 0xFFFFu);
+            if (nn == 0 && compat) {
+                const unsigned long long key = *first_key;
+                const int32_t p0 = key == ~0ull ? 0 : (int32_t)(key & ((1ull << 21) - 1));
+                const int32_t* Tp = d.T + (int64_t)p0 * d.t_cols;
+                s = 0.0 + 1.0 / (double)(Tp[tca] + Tp[d.tcol_col[b]] - 1);
+                nn = 1;
+            }
+            if (aji) aji[idx] = nn ? s / (double)nn : 0.0;
+            if (s_out) s_out[idx] = s;
+            if (n_out) n_out[idx] = nn;
         }
     }
 }
