@@ -42,6 +42,7 @@ struct pfaai_ctx {
     // device-resident problem
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
     bool has_g = false;
+    bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
     Dev dev{};
 
     // work space (sized at load for all rows, so runs never allocate)
@@ -61,7 +62,7 @@ struct pfaai_ctx {
 
 namespace {
 
-constexpr int kDefaultRowsVariant = 3;  // k_rows: 2 WGs/CU, 4 ranges in flight per group, no tail queue
+constexpr int kDefaultRowsVariant = 11;  // fused genome-major k_rows (variant 3 without G lists)
 
 // scalars buffer layout (u64 each)
 enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
@@ -205,15 +206,34 @@ int build_records_g(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool fi
     hipLaunchKernelGGL(k_glen, dim3(ceil_div(K, 256)), dim3(256), 0, s, c->dev, rb, K, len);
     int rc = scan_u32(c, len, K, rowptr, s);
     if (rc) return rc;
+    const size_t glds = 0;
     if (c->recs_batch == 0 && MODE == 0)
-        hipLaunchKernelGGL((k_recs_g<MODE, 0>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+        hipLaunchKernelGGL((k_recs_g<MODE, 0>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
                            static_cast<uint2*>(c->recs.p));
     else if (c->recs_batch == 8)
-        hipLaunchKernelGGL((k_recs_g<MODE, 8>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+        hipLaunchKernelGGL((k_recs_g<MODE, 8>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
                            static_cast<uint2*>(c->recs.p));
     else
-        hipLaunchKernelGGL((k_recs_g<MODE, 1>), dim3(re - rb), dim3(kTetraThreads), 0, s, c->dev, rb, rowptr,
+        hipLaunchKernelGGL((k_recs_g<MODE, 1>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
                            static_cast<uint2*>(c->recs.p));
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_OK;
+}
+
+// Fused genome-major path: only the run table (+ the first E triple for the
+// ref-compat zero-overlap quirk); k_rows walks the G lists itself.
+template <int MODE>
+int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    HIPCHK(c, hipMemsetAsync(c->blk.p, 0, c->blk.bytes, s));
+    hipLaunchKernelGGL(k_blk, dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, err);
+    if (first_event) {
+        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
+                           (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
+                           static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
+    }
     HIPCHK(c, hipGetLastError());
     return PFAAI_OK;
 }
@@ -244,8 +264,22 @@ void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
     auto* recs = static_cast<const uint2*>(c->recs.p);
-    if (c->occupancy == 2)
+    if (c->occupancy >= 9) {
+        if (!c->has_g) return;  // checked by run_mode
+        if (c->occupancy == 11)
+            hipLaunchKernelGGL((k_rows<MODE, KW, 11>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
+                               rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+        else if (c->occupancy == 9)
+            hipLaunchKernelGGL((k_rows<MODE, KW, 9>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                               rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+        else
+            hipLaunchKernelGGL((k_rows<MODE, KW, 10>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
+                               rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    } else if (c->occupancy == 2)
         hipLaunchKernelGGL((k_rows<MODE, KW, 2>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 8)
+        hipLaunchKernelGGL((k_rows<MODE, KW, 8>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     else if (c->occupancy == 7)
         hipLaunchKernelGGL((k_rows<MODE, KW, 7>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev, rb,
@@ -282,6 +316,38 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     }
 }
 
+// Work-list space for the sorted (F-only) and searched (G, variants <= 8)
+// paths, sized for all rows: ~36 B per F entry of the row genomes.  The
+// default genome-major path (fused k_rows) needs none of it, so it is
+// allocated at load only for F-only input and otherwise on first use.
+int ensure_worklists(pfaai_ctx* c) {
+    if (c->wl_ready) return PFAAI_OK;
+    const auto& p = c->prob;
+    int rc;
+    const int64_t nmax = std::max<int64_t>(1, c->row_fprefix[c->n_rows]);
+    const int64_t K = c->n_rows * p.n_prot;
+    const int64_t ntiles = ceil_div(nmax, kRsTile);
+    const int64_t hist_n = kRsBins * ntiles;
+    if ((rc = ensure(c, c->rowptr, (K + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->lens, std::max<int64_t>(K, 1) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->off_t, (PFAAI_NTETRAMERS + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->key_c, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->rec_c, nmax * sizeof(uint2)))) return rc;
+    if ((rc = ensure(c, c->key_a, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->key_b, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->val_a, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->val_b, nmax * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->recs, nmax * sizeof(uint2)))) return rc;
+    if ((rc = ensure(c, c->hist, hist_n * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c, c->hoff, (hist_n + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max({hist_n, K, (int64_t)PFAAI_NTETRAMERS}), kScanTile)) *
+                                     sizeof(unsigned long long))))
+        return rc;
+    c->wl_ready = true;
+    return PFAAI_OK;
+}
+
 template <int MODE>
 int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
              hipStream_t s) {
@@ -300,7 +366,14 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     c->ev1 = ev[1];
     c->ev2 = ev[2];
     HIPCHK(c, hipEventRecord(c->ev0, s));
-    int rc = c->has_g ? build_records_g<MODE>(c, rb, re, s, compat) : build_records<MODE>(c, rb, re, s, compat);
+    const bool fused = c->has_g && c->occupancy >= 9;
+    if (!fused) {
+        const int rcw = ensure_worklists(c);
+        if (rcw) return rcw;
+    }
+    int rc = fused     ? build_runs_g<MODE>(c, s, compat)
+             : c->has_g ? build_records_g<MODE>(c, rb, re, s, compat)
+                        : build_records<MODE>(c, rb, re, s, compat);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
@@ -466,7 +539,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
                 return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
         if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
         if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
-        if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint2)))) return rc;
+        if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     }
 
     Dev& d = c->dev;
@@ -490,7 +563,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
     d.G_off = c->has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
     d.G_tet = c->has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
-    d.blk = c->has_g ? static_cast<uint2*>(c->blk.p) : nullptr;
+    d.blk = c->has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
 
     // Work space sized for all rows, so pfaai_run never allocates or syncs.
     // Work-list entries of a row = F entries of its genome (counted here).
@@ -510,27 +583,9 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
             }
         }
     }
-    const int64_t nmax = std::max<int64_t>(1, c->row_fprefix[c->n_rows]);
-    const int64_t K = c->n_rows * p.n_prot;
-    const int64_t ntiles = ceil_div(nmax, kRsTile);
-    const int64_t hist_n = kRsBins * ntiles;
-    if ((rc = ensure(c, c->rowptr, (K + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->lens, std::max<int64_t>(K, 1) * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->off_t, (PFAAI_NTETRAMERS + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->key_c, nmax * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->rec_c, nmax * sizeof(uint2)))) return rc;
-    if ((rc = ensure(c, c->key_a, nmax * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->key_b, nmax * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->val_a, nmax * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->val_b, nmax * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->recs, nmax * sizeof(uint2)))) return rc;
-    if ((rc = ensure(c, c->hist, hist_n * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c, c->hoff, (hist_n + 1) * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max({hist_n, K, (int64_t)PFAAI_NTETRAMERS}), kScanTile)) *
-                                     sizeof(unsigned long long))))
-        return rc;
     HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
+    c->wl_ready = false;
+    if (!c->has_g && (rc = ensure_worklists(c))) return rc;
     c->loaded = true;
     return PFAAI_OK;
 }
@@ -579,7 +634,8 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     {
         const char* occ = getenv("PFAAI_ROWS_OCC");
         const int v = occ ? atoi(occ) : 0;
-        c->occupancy = (v >= 1 && v <= 7) ? v : kDefaultRowsVariant;
+        c->occupancy = (v >= 1 && v <= 11) ? v : kDefaultRowsVariant;
+        if (c->occupancy >= 9 && !c->has_g) c->occupancy = 3;  // fused variants walk the G lists
         const char* rbv = getenv("PFAAI_RECS_BATCH");
         const int r = rbv ? atoi(rbv) : 1;
         c->recs_batch = (r == 0 || r == 8) ? r : 1;
@@ -673,6 +729,7 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
     const int64_t cells = (int64_t)p.n_prot * p.n_ids;
     int rc;
     if ((rc = ensure(c, c->dbg, cells * sizeof(int32_t)))) return rc;
+    if ((rc = ensure_worklists(c))) return rc;
     HIPCHK(c, hipMemsetAsync(c->dbg.p, 0, cells * sizeof(int32_t), c->stream));
     const int32_t chunk = 2 * 10 * kRowThreads;
     const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);

@@ -35,6 +35,8 @@ constexpr int kMaxRuns = 4096;          // proteins per tetramer block (checked 
 constexpr int kRowThreads = 1024;       // K-S+J workgroup (16 waves)
 constexpr int kGroup = 16;              // lanes per member range in the scatter
 constexpr int kNumGroups = kRowThreads / kGroup;
+constexpr int kSplitters = 3, kSplitBits = 21;  // run-line splitters in blk (genome ids < 2^21)
+constexpr uint64_t kSplitNone = (1ull << kSplitBits) - 1;
 
 // Device view of a loaded problem (pfaai_problem + derived maps).
 struct Dev {
@@ -53,7 +55,7 @@ struct Dev {
     const int32_t* tcol_col;    // [n_ids] T column used when the genome is genomeB
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
-    uint2* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run [start, end)
+    uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
 };
 
 // XCD-aware row order (MI355X_MICROARCH.md: workgroups are dealt round-robin
@@ -272,7 +274,10 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 // ---------------------------------------------------------------------------
 // K-W1g (genome-major input): run table + work lists without any sort.
 //   k_blk:    one workgroup per tetramer block: run heads by wavefront ballot,
-//             blk[p * 160000 + t] = [start, end) of run (t, p) in F.
+//             blk[p * 160000 + t] = {start, end, splitters} of run (t, p)
+//             in F; the splitters are the genome ids at the run's 64-B line
+//             boundaries 1..3 (21 bits each, 0x1FFFFF past the end), which
+//             let a row skip whole lines outside its column window.
 //   k_glen:   work-list length of every (row, protein) = its G list length.
 //   k_recs_g: one workgroup per output row; each G entry (A, p, t) of the
 //             row looks up its run and becomes the member range of A in it:
@@ -320,7 +325,16 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int* __restrict__ 
         __syncthreads();
         for (int j = tid; j < nr; j += kTetraThreads) {
             const int64_t rs = s + runs[j], re = s + runs[j + 1];
-            d.blk[(int64_t)d.Fp[rs] * kNTetramers + t] = make_uint2((uint32_t)rs, (uint32_t)re);
+            const int64_t first = rs & ~(int64_t)(kGroup - 1);
+            uint64_t sp = 0;
+#pragma unroll
+            for (int i = 1; i <= kSplitters; ++i) {
+                const int64_t m = first + (int64_t)i * kGroup;
+                const uint64_t v = m < re ? (uint64_t)d.Fg[m] : kSplitNone;
+                sp |= v << (kSplitBits * (i - 1));
+            }
+            d.blk[(int64_t)d.Fp[rs] * kNTetramers + t] =
+                make_uint4((uint32_t)rs, (uint32_t)re, (uint32_t)sp, (uint32_t)(sp >> 32));
         }
         __syncthreads();
     }
@@ -343,6 +357,9 @@ template <int MODE, int kRecsBatchT>
 __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_begin,
                                                           const unsigned long long* __restrict__ rowptr,
                                                           uint2* __restrict__ recs) {
+    // static 32 KiB on purpose: it caps k_recs_g at 5 workgroups per CU, which
+    // measured faster (11.3 ms vs 16.8 ms at 10k) than full occupancy -- the
+    // run searches thrash L2 with more rows in flight
     __shared__ long long goff[kMaxRuns + 1];
     const int tid = threadIdx.x;
     const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
@@ -373,7 +390,8 @@ __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_beg
         for (int u = 0; u < kRecsBatch; ++u) t[u] = live[u] ? d.G_tet[kb + (int64_t)u * kTetraThreads] : 0;
 #pragma unroll
         for (int u = 0; u < kRecsBatch; ++u) {
-            const uint2 run = live[u] ? d.blk[(int64_t)pr[u] * kNTetramers + t[u]] : make_uint2(0u, 0u);
+            const uint4 r4 = live[u] ? d.blk[(int64_t)pr[u] * kNTetramers + t[u]] : make_uint4(0u, 0u, 0u, 0u);
+            const uint2 run = make_uint2(r4.x, r4.y);
             lo[u] = run.x;
             hi[u] = run.y;
             end[u] = run.y;
@@ -414,7 +432,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_beg
                 } else if constexpr (MODE == 1) {
                     rec = make_uint2(lo[u], end[u]);
                 } else {
-                    const uint2 run = d.blk[(int64_t)pr[u] * kNTetramers + t[u]];
+                    const uint4 run = d.blk[(int64_t)pr[u] * kNTetramers + t[u]];
                     rec = make_uint2(run.x, lo[u]);
                 }
             }
@@ -711,6 +729,113 @@ __device__ __forceinline__ uint32_t scatter_row_protein(const Dev& d, int32_t a,
     return ev;
 }
 
+// ---------------------------------------------------------------------------
+// Fused genome-major scatter (k_rows OCC 9): no work list at all.  The rows'
+// (row, protein) member ranges are exactly the runs (t, p) of the row
+// genome's own G entries (A, p, t) -- A is a member of each -- and the order
+// of ranges inside one protein does not matter to the integer counts.  So per
+// protein the workgroup stages run = blk[p][t] for its G entries in LDS,
+// cuts every run into 64-B-aligned 16-member "line tasks" (one block scan
+// gives both a run's task offset and, for runs longer than kMaxLines lines,
+// its slot in the whole-workgroup queue), and each 16-lane group takes
+// kUnroll tasks at a time with their loads in flight together.  Members
+// outside the row's column window (B <= A for ALL, queries for QT) or not a
+// valid QSUB partner are dropped by scatter_one, exactly as before -- the
+// member position of A is never searched for.
+// ---------------------------------------------------------------------------
+constexpr int kMaxLines = 8;                       // lines a run may hand out as tasks
+constexpr int kTaskCap = kMaxLines * kRowThreads;  // u16 tasks: (run slot | line << 10)
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+template <int MODE, int kUnroll, bool PRUNE>
+__device__ __forceinline__ uint32_t scatter_row_g(const Dev& d, int32_t a, int p, int64_t gb, int64_t ge,
+                                                  uint32_t* acc, uint2* rec_lds, uint16_t* task_lds,
+                                                  uint32_t* wsum, uint2* long_lds, int32_t cc0, int32_t cc1) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int grp = tid / kGroup, gl = tid % kGroup;
+    const uint4* blk_p = d.blk + (int64_t)p * kNTetramers;
+    uint32_t ev = 0;
+    for (int64_t base = gb; base < ge; base += kRowThreads) {  // uniform trip count
+        const int n = (int)(ge - base < kRowThreads ? ge - base : kRowThreads);
+        __syncthreads();  // previous readers of the staging arrays are done
+        uint4 r4 = make_uint4(0u, 0u, 0u, 0u);
+        if (tid < n) r4 = blk_p[d.G_tet[base + tid]];
+        uint2 r = make_uint2(r4.x, r4.y);
+        // a run of one member is A alone: no partner
+        const uint32_t first = r.x & ~(uint32_t)(kGroup - 1);
+        uint32_t nl = r.y - r.x > 1u ? (r.y - first + kGroup - 1) / kGroup : 0u;
+        if (PRUNE && nl > 1u) {  // lines [l0, l1) can hold members in [cc0, cc1)
+            const uint64_t sp = (uint64_t)r4.z | ((uint64_t)r4.w << 32);
+            uint32_t l0 = 0, l1 = nl;
+#pragma unroll
+            for (uint32_t i = 1; i <= (uint32_t)kSplitters; ++i) {
+                const int32_t f = (int32_t)((sp >> (kSplitBits * (i - 1))) & kSplitNone);
+                if (i < nl) {
+                    if (f <= cc0) l0 = i;               // lines < i hold ids < f <= cc0
+                    if (f >= cc1 && l1 > i) l1 = i;     // lines >= i hold ids >= f >= cc1
+                }
+            }
+            if (l1 <= l0) { nl = 0; }
+            else {
+                if (l0) r.x = first + l0 * kGroup;
+                if (l1 < nl) r.y = first + l1 * kGroup;
+                nl = l1 - l0;
+            }
+        }
+        const bool lng = nl > (uint32_t)kMaxLines;
+        const uint32_t v = lng ? (1u << 16) : nl;  // low half: tasks, high half: long runs
+        rec_lds[tid] = r;
+        const uint32_t inc = wave_incl_scan_u32(v);
+        if (lane == 63) wsum[wid] = inc;
+        __syncthreads();
+        // wave offsets: lane w < 16 holds wave w's total; scan them across the lanes
+        const uint32_t ws = wave_incl_scan_u32(lane < kRowThreads / 64 ? wsum[lane] : 0u);
+        const uint32_t off = wid ? (uint32_t)__shfl(ws, wid - 1, 64) : 0u;
+        const uint32_t tot = (uint32_t)__shfl(ws, kRowThreads / 64 - 1, 64);
+        const uint32_t ex = off + inc - v;
+        if (lng) long_lds[ex >> 16] = r;
+        else
+            for (uint32_t i = 0; i < nl; ++i) task_lds[(ex & 0xFFFFu) + i] = (uint16_t)(tid | (i << 10));
+        const int n_tasks = (int)(tot & 0xFFFFu), n_long = (int)(tot >> 16);
+        __syncthreads();
+        for (int j = grp; j < n_tasks; j += kNumGroups * kUnroll) {
+            int32_t b[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int k = j + u * kNumGroups;
+                b[u] = -1;
+                if (k < n_tasks) {
+                    const uint32_t tk = task_lds[k];
+                    const uint2 rr = rec_lds[tk & 1023u];
+                    const uint32_t m = (rr.x & ~(uint32_t)(kGroup - 1)) + (tk >> 10) * kGroup + gl;
+                    if (m >= rr.x && m < rr.y) b[u] = d.Fg[m];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) scatter_one<MODE>(d, a, b[u], acc, cc0, cc1, ev);
+        }
+        for (int q = 0; q < n_long; ++q) {  // e.g. a core tetramer shared by every genome
+            const uint2 rr = long_lds[q];
+            for (uint32_t m = rr.x + tid; m < rr.y; m += kRowThreads) scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
+        }
+    }
+    return ev;
+}
+
+template <int MODE, int kUnroll>
+__device__ __forceinline__ uint32_t scatter_row_rle(const Dev& d, int32_t a, const uint2* __restrict__ recs,
+                                                    uint64_t rb, uint64_t re, uint32_t* acc, uint2* rec_lds,
+                                                    int32_t cc0, int32_t cc1);
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -732,8 +857,11 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
     unsigned long long* __restrict__ n_events) {
     extern __shared__ uint32_t acc[];  // KW*1024 counter words (+ OCC 7: a u16 T row of 2*KW*1024)
+    constexpr bool kFusedG = OCC == 9 || OCC == 10 || OCC == 11;  // genome-major fused scatter (no work list)
     __shared__ uint2 rec_lds[kRowThreads];
-    __shared__ uint2 long_lds[OCC == 7 || OCC == 6 ? 1 : kRowThreads];
+    __shared__ uint2 long_lds[OCC == 7 || OCC == 6 || OCC == 3 || OCC == 8 ? 1 : kRowThreads];
+    __shared__ uint16_t task_lds[kFusedG ? kTaskCap : 1];
+    __shared__ uint32_t wsum[kRowThreads / 64];
     __shared__ int n_long;
     uint16_t* trow = reinterpret_cast<uint16_t*>(acc + KW * kRowThreads);
     const int tid = threadIdx.x;
@@ -758,7 +886,14 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
     __syncthreads();
 
     for (int p = 0; p < P; ++p) {
-        const uint64_t rb = rowptr[rl * P + p], re = rowptr[rl * P + p + 1];
+        uint64_t rb, re;
+        if constexpr (kFusedG) {
+            rb = (uint64_t)d.G_off[(int64_t)a * P + p];
+            re = (uint64_t)d.G_off[(int64_t)a * P + p + 1];
+        } else {
+            rb = rowptr[rl * P + p];
+            re = rowptr[rl * P + p + 1];
+        }
         if (rb == re) continue;  // uniform: no E triple (p, a, *)
         if (OCC == 7) {  // stage this protein's T row (u16) for the chunk's columns; read after the barrier
             const int32_t* Tq = d.T + (int64_t)p * d.t_cols;
@@ -766,11 +901,14 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
                 trow[c] = (uint16_t)Tq[compat ? d.tcol_col[cc0 + c] : cc0 + c];
         }
         if (flags & 0x200u) {  // diagnostics: 0x200 skips the scatter
+        } else if constexpr (kFusedG) {
+            ev += scatter_row_g<MODE, OCC == 9 ? 4 : 8, OCC == 11>(d, a, p, (int64_t)rb, (int64_t)re, acc, rec_lds, task_lds,
+                                                         wsum, long_lds, cc0, cc1);
         } else if (OCC == 6 || OCC == 7) {
             ev += scatter_row_rle<MODE, 4>(d, a, recs, rb, re, acc, rec_lds, cc0, cc1);
         } else {
-            ev += scatter_row_protein<MODE, OCC == 1 ? 8 : 4, OCC != 3>(d, a, recs, rb, re, acc, rec_lds, long_lds,
-                                                                        &n_long, cc0, cc1);
+            ev += scatter_row_protein<MODE, (OCC == 1 || OCC == 8) ? 8 : 4, OCC != 3 && OCC != 8>(
+                d, a, recs, rb, re, acc, rec_lds, long_lds, &n_long, cc0, cc1);
         }
         __syncthreads();
         if (flags & 0x100u) {  // diagnostics: 0x100 skips the normalisation (counters just cleared)

@@ -1,0 +1,93 @@
+"""Summarise rocprofv3 --pmc passes (tools/gpu/pmc.sh) per kernel.
+
+Reads <dir>/p*/run_counter_collection.csv (one counter group per pass, each
+over the same 10k all-vs-all run), averages every counter over the dispatches
+of each kernel, derives the ratios DESIGN.md quotes, and writes
+
+  profiles/<tag>_pmc.json   -- every kernel, every counter, derived ratios
+  profiles/pmc_k_rows.json  -- HBM bytes per k_rows launch (bench.py's
+                               roofline.traffic)
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3):
+FETCH_SIZE and WRITE_SIZE are in KiB; the x2 gfx950 FETCH correction is
+calibrated only for 16-B-per-lane streaming reads.  k_rows' reads are 4-8 B
+gathers (member ids, work records, T entries), so the raw figure is used and
+the x2 figure is recorded next to it as an upper bound.
+
+usage: python tools/pmc_summary.py gpurun_out/pmc r01
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.split("(")[0]
+    for pre in ("void ",):
+        if n.startswith(pre):
+            n = n[len(pre):]
+    return n
+
+
+def collect(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} | {"_dispatches": max(len(v) for v in cs.values())}
+            for k, cs in acc.items()}
+
+
+def derive(c):
+    out = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["hbm_read_bytes"] = c["FETCH_SIZE"] * 1024
+        out["hbm_read_bytes_x2_bound"] = 2 * c["FETCH_SIZE"] * 1024
+        out["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
+        out["hbm_bytes"] = out["hbm_read_bytes"] + out["hbm_write_bytes"]
+    if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+        out["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if c.get("SQ_WAVE_CYCLES", 0) > 0:
+        w = c["SQ_WAVE_CYCLES"]
+        out["wave_frac_waiting"] = c.get("SQ_WAIT_ANY", 0) / w
+        out["wave_frac_issue_stall"] = c.get("SQ_WAIT_INST_ANY", 0) / w
+        out["wave_frac_active"] = c.get("SQ_ACTIVE_INST_ANY", 0) / w
+    if c.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
+        out["lds_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
+    return out
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    ks = collect(d)
+    if not ks:
+        sys.exit(f"no counter CSVs under {d}")
+    res = {k: {"counters": c, "derived": derive(c)} for k, c in ks.items() if k.startswith("pfaai::") or "pfaai::" in k}
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
+        json.dump({"source": "rocprofv3 --pmc --kernel-trace, tools/gpu/pmc.sh, 10k SYN all-vs-all",
+                   "kernels": res}, f, indent=1, sort_keys=True)
+    rows = [k for k in res if "k_rows" in k]
+    if rows:
+        k = rows[0]
+        dv = res[k]["derived"]
+        with open(os.path.join(prof, "pmc_k_rows.json"), "w") as f:
+            json.dump({"kernel": k, "hbm_bytes_per_launch": dv.get("hbm_bytes"),
+                       "hbm_read_bytes_x2_bound": dv.get("hbm_read_bytes_x2_bound"),
+                       "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, one launch covers all 10k rows",
+                       "tag": tag}, f, indent=1)
+    for k, v in res.items():
+        dv = v["derived"]
+        print(f"{k:40s} " + " ".join(f"{n}={x:.4g}" for n, x in dv.items()))
+
+
+if __name__ == "__main__":
+    main()
