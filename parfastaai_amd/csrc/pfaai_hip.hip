@@ -14,6 +14,8 @@
 
 #include "pfaai_hip.h"
 #include "pfaai_kernels.hpp"
+#include "pfaai_rows_pl.hpp"
+#include "pfaai_counts.hpp"
 
 using namespace pfaai;
 
@@ -40,6 +42,13 @@ struct pfaai_ctx {
     int32_t max_cols = 0;
 
     // device-resident problem
+    DevBuf T16, T16c;
+    // two-phase row path (variant 13): per-row cell bases of the count tensor
+    std::vector<unsigned long long> cbase_h;
+    DevBuf cbase, counts;
+    int32_t cnt_chunks = 1;
+    size_t cnt_budget = 0;
+    int64_t max_glen = 0;  // longest (genome, protein) G list
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
     bool has_g = false;
     bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
@@ -62,7 +71,9 @@ struct pfaai_ctx {
 
 namespace {
 
-constexpr int kDefaultRowsVariant = 11;  // fused genome-major k_rows (variant 3 without G lists)
+constexpr int kDefaultRowsVariant = 11;  // fused genome-major k_rows (fastest measured: 19.3 ms at 10k)
+constexpr int64_t kPlMaxGlen = kRowThreads;
+constexpr size_t P_SLAB_MAX = (size_t)3 << 30;  // bytes of one protein's count slab (< 4 GiB)  // k_rows_pl: G list entries per (genome, protein)
 
 // scalars buffer layout (u64 each)
 enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
@@ -301,9 +312,108 @@ void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
+// k_rows_pl (variant 12): KW <= 5 counter words per thread, wider rows are
+// cut into chunks of 10 240 columns starting at even columns.
+template <int MODE, int KW>
+void launch_rows_pl_kw(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                       hipStream_t s) {
+    const int32_t chunk = 2 * KW * kRowThreads;
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const size_t lds = (2 * (size_t)KW * kRowThreads + c->prob.n_prot + 1) * sizeof(uint32_t);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    if (c->occupancy == 14)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 16>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 15)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 12>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 8>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+}
+
+template <int MODE>
+void launch_rows_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                    hipStream_t s) {
+    const int64_t words = ceil_div((int64_t)c->max_cols + 1, 2);
+    if (words <= 1 * kRowThreads) launch_rows_pl_kw<MODE, 1>(c, rb, re, flags, aji, S, N, s);
+    else if (words <= 2 * kRowThreads) launch_rows_pl_kw<MODE, 2>(c, rb, re, flags, aji, S, N, s);
+    else if (words <= 3 * kRowThreads) launch_rows_pl_kw<MODE, 3>(c, rb, re, flags, aji, S, N, s);
+    else if (words <= 4 * kRowThreads) launch_rows_pl_kw<MODE, 4>(c, rb, re, flags, aji, S, N, s);
+    else launch_rows_pl_kw<MODE, 5>(c, rb, re, flags, aji, S, N, s);
+}
+
+// Two-phase row path (variant 13): rows are cut into tiles whose count
+// tensor (P x cells x 2 B) fits the budget; per tile k_counts then k_norm.
+template <int MODE>
+int launch_rows_2p(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                   hipStream_t s) {
+    const int64_t P = c->prob.n_prot;
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    const auto* cb = static_cast<const unsigned long long*>(c->cbase.p);
+    const auto& h = c->cbase_h;
+    int64_t t0 = rb;
+    while (t0 < re) {
+        // largest tile from t0 within the budget (at least one row)
+        int64_t t1 = t0 + 1;
+        {
+            int64_t lo = t0 + 1, hi = re;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) / 2;
+                if ((h[mid] - h[t0]) * 2 * (uint64_t)P <= c->cnt_budget) lo = mid; else hi = mid - 1;
+            }
+            t1 = lo;
+        }
+        const uint64_t cells = h[t1] - h[t0];
+        const uint64_t pitch = cells / 2;  // words per protein
+        int rc = ensure(c, c->counts, std::max<uint64_t>(pitch * P * 4, 16));
+        if (rc) return rc;
+        auto* cnt = static_cast<uint32_t*>(c->counts.p);
+        const int64_t rows = t1 - t0;
+        const int64_t groups = (rows + kCntRowGroup - 1) / kCntRowGroup;
+        const int64_t total = groups * kCntRowGroup * c->cnt_chunks * P;
+        const int64_t grid = ceil_div(total, kXcds) * kXcds;
+        unsigned long long* prof = nullptr;  // diagnostics: PFAAI_PROF_COUNTS=1 prints k_counts stage clocks
+        if (getenv("PFAAI_PROF_COUNTS")) {
+            if ((rc = ensure(c, c->dbg, 8 * sizeof(unsigned long long)))) return rc;
+            prof = static_cast<unsigned long long*>(c->dbg.p);
+            HIPCHK(c, hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s));
+        }
+        const char* abl = getenv("PFAAI_CNT_ABLATE");  // diagnostics: bit 0 no atomics, bit 1 no member loads
+        const uint32_t dbg = abl ? (uint32_t)atoi(abl) : 0u;
+        const char* pad = getenv("PFAAI_CNT_LDS_PAD");  // diagnostics: extra LDS per workgroup (KiB) -> occupancy
+        const size_t padb = pad ? (size_t)atoi(pad) << 10 : 0;
+        hipLaunchKernelGGL((k_counts<MODE>), dim3((unsigned)grid), dim3(kCntThreads), padb, s, c->dev, t0, (int32_t)rows,
+                           c->cnt_chunks, cb, (uint64_t)pitch, cnt, sc + SC_EVENTS, prof, dbg);
+        if (prof) {
+            unsigned long long h8[8];
+            HIPCHK(c, hipMemcpyAsync(h8, prof, sizeof(h8), hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const char* nm[8] = {"setup", "G+blk", "tasks", "barrier1", "scatter", "whole", "barrier2", "store"};
+            double tot = 0;
+            for (int k = 0; k < 8; ++k) tot += (double)h8[k];
+            for (int k = 0; k < 8; ++k)
+                fprintf(stderr, "k_counts %-9s %6.1f %%  %.0f cyc/item-pass\n", nm[k], 100.0 * h8[k] / tot,
+                        (double)h8[k] / (double)total);
+        }
+        hipLaunchKernelGGL((k_norm<MODE>), dim3((unsigned)rows), dim3(kNormThreads), P * sizeof(int32_t), s, c->dev, t0,
+                           cb, (uint64_t)pitch, (const uint32_t*)cnt, flags, sc + SC_FIRST_KEY, aji, S, N);
+        t0 = t1;
+    }
+    return PFAAI_OK;
+}
+
 template <int MODE>
 void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S,
                  int32_t* N, hipStream_t s) {
+    if (c->occupancy == 13) {
+        (void)launch_rows_2p<MODE>(c, rb, re, flags, aji, S, N, s);
+        return;
+    }
+    if (c->occupancy == 12 || c->occupancy == 14 || c->occupancy == 15) {
+        launch_rows_pl<MODE>(c, rb, re, flags, aji, S, N, s);
+        return;
+    }
     const int kw = pick_kw(c->max_cols);
     const int32_t chunk = 2 * kw * kRowThreads;
     const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
@@ -415,7 +525,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     if (!c) return PFAAI_OK;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
+    for (DevBuf* b : {&c->T16, &c->T16c, &c->cbase, &c->counts, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
@@ -526,6 +636,24 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     if ((rc = upload(c, c->tcol_row, tcol_row.data(), ni))) return rc;
     if ((rc = upload(c, c->tcol_col, tcol_col.data(), ni))) return rc;
 
+    // u16 T by column genome id (and through tcol_col for the QT quirk), rows
+    // of an even number of columns so one u32 holds a counter word's pair
+    c->dev.t16_cols = ((int64_t)ni + 15) & ~(int64_t)7;  // 16-B rows, >= n_ids + 8 (uint4 reads past chi)
+    {
+        const int64_t tc = c->dev.t16_cols;
+        std::vector<uint16_t> t16((size_t)p.n_prot * tc, 0);
+        for (int64_t q = 0; q < p.n_prot; ++q)
+            for (int32_t g = 0; g < ni; ++g) t16[q * tc + g] = (uint16_t)p.T[q * p.t_cols + g];
+        if ((rc = upload(c, c->T16, t16.data(), t16.size()))) return rc;
+        if (p.mode == PFAAI_MODE_QT) {
+            for (int64_t q = 0; q < p.n_prot; ++q)
+                for (int32_t g = 0; g < ni; ++g) t16[q * tc + g] = (uint16_t)p.T[q * p.t_cols + tcol_col[g]];
+            if ((rc = upload(c, c->T16c, t16.data(), t16.size()))) return rc;
+        } else {
+            release(c->T16c);
+        }
+    }
+
     c->has_g = p.G_off && p.G_tet;
     if (c->has_g) {
         const int64_t ng = (int64_t)ni * p.n_prot;
@@ -537,6 +665,8 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         for (int64_t k = 0; k < gt; ++k)
             if (p.G_tet[k] < 0 || p.G_tet[k] >= PFAAI_NTETRAMERS)
                 return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
+        c->max_glen = 0;
+        for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, p.G_off[k + 1] - p.G_off[k]);
         if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
         if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
@@ -564,6 +694,8 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     d.G_off = c->has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
     d.G_tet = c->has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
     d.blk = c->has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
+    d.T16 = static_cast<const uint16_t*>(c->T16.p);
+    d.T16c = c->T16c.p ? static_cast<const uint16_t*>(c->T16c.p) : d.T16;
 
     // Work space sized for all rows, so pfaai_run never allocates or syncs.
     // Work-list entries of a row = F entries of its genome (counted here).
@@ -582,6 +714,23 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
                 c->row_fprefix[r + 1] = c->row_fprefix[r] + (p.G_off[g0 + p.n_prot] - p.G_off[g0]);
             }
         }
+    }
+    // count-tensor cell layout: row r covers columns [clo & ~7, chi) padded to 8 cells
+    {
+        c->cbase_h.assign(c->n_rows + 1, 0);
+        int64_t maxc = 0;
+        for (int64_t r = 0; r < c->n_rows; ++r) {
+            const int32_t g = c->row_genome_h[r];
+            int64_t lo, hi;
+            if (p.mode == PFAAI_MODE_ALL) { lo = g + 1; hi = ni; }
+            else if (p.mode == PFAAI_MODE_QSUB) { lo = 0; hi = ni; }
+            else { lo = 0; hi = p.n_tgt; }
+            const int64_t cells = hi > lo ? ((hi - (lo & ~7LL) + 7) & ~7LL) : 0;
+            maxc = std::max(maxc, cells);
+            c->cbase_h[r + 1] = c->cbase_h[r] + cells;
+        }
+        c->cnt_chunks = (int32_t)std::max<int64_t>(1, ceil_div(maxc, 2 * kCntChunkW));
+        if ((rc = upload(c, c->cbase, c->cbase_h.data(), c->cbase_h.size()))) return rc;
     }
     HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
     c->wl_ready = false;
@@ -634,7 +783,13 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     {
         const char* occ = getenv("PFAAI_ROWS_OCC");
         const int v = occ ? atoi(occ) : 0;
-        c->occupancy = (v >= 1 && v <= 11) ? v : kDefaultRowsVariant;
+        c->occupancy = (v >= 1 && v <= 15) ? v : kDefaultRowsVariant;
+        if ((c->occupancy == 12 || c->occupancy >= 14) && c->max_glen > kPlMaxGlen) c->occupancy = 11;  // lists too long to pipeline
+        if (c->occupancy == 13 && !c->has_g) c->occupancy = 3;
+        const char* bud = getenv("PFAAI_COUNT_BUDGET_MB");  // count-tensor budget of the two-phase path
+        c->cnt_budget = (size_t)(bud ? atoll(bud) : 16384) << 20;
+        // a protein's slab is addressed with 32-bit offsets in k_norm
+        c->cnt_budget = std::min<size_t>(c->cnt_budget, (size_t)P_SLAB_MAX * (size_t)c->prob.n_prot);
         if (c->occupancy >= 9 && !c->has_g) c->occupancy = 3;  // fused variants walk the G lists
         const char* rbv = getenv("PFAAI_RECS_BATCH");
         const int r = rbv ? atoi(rbv) : 1;

@@ -56,6 +56,9 @@ struct Dev {
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
+    const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)
+    const uint16_t* T16c;       // same through tcol_col (ref-compat QT quirk); == T16 otherwise
+    int64_t t16_cols;           // even, >= n_ids
 };
 
 // XCD-aware row order (MI355X_MICROARCH.md: workgroups are dealt round-robin

@@ -35,7 +35,8 @@ def _newer(out, srcs):
 
 def build_hip(force=False):
     src = os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_hip.hip")
-    deps = [src, os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_kernels.hpp"), os.path.join(ROOT, "include/pfaai_hip.h")]
+    csrc = os.path.join(ROOT, "parfastaai_amd/csrc")
+    deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include/pfaai_hip.h")]
     out = os.path.join(ROOT, "parfastaai_amd/lib/libpfaai_hip.so")
     if force or _newer(out, deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
