@@ -45,6 +45,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
+ROWS_KERNEL = "pfaai::k_rows_pl (fused scatter + Jaccard + AJI, default row kernel)"
 
 
 def log(msg):
@@ -218,7 +219,7 @@ def main():
         step_bytes = 8 * total_events + 4 * n_f + 8 * n_pairs  # SURVEY §8d B_alg
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(),
-                    "kernel": "pfaai::k_rows (scatter + Jaccard + AJI)",
+                    "kernel": ROWS_KERNEL,
                     "kernel_ms": round(k_rows_ms, 4), "alg_bytes_per_launch": alg_bytes,
                     "build_kernels_ms": round(ms_build / max(n_runs, 1), 4)}
         cpu = None

@@ -148,6 +148,12 @@ int pfaai_timing(pfaai_ctx* ctx, int reset, int32_t* n_runs, double* ms_build,
  * the reference's sorted E (ds_helper.hpp:414-418) restricted to genomeA. */
 int pfaai_debug_row_counts(pfaai_ctx* ctx, int64_t row, int32_t* h_counts);
 
+/* Self-test of the row kernels' exact small-integer division: compares
+ * c / d computed by the fast path with IEEE '/' for every 1 <= c <= c_max,
+ * c <= d <= d_max on the device; *mismatches receives the count (0 = every
+ * quotient bit-identical). */
+int pfaai_debug_div_check(pfaai_ctx* ctx, int32_t c_max, int32_t d_max, int64_t* mismatches);
+
 /* Device memory helpers (so callers without a GPU framework can run the
  * device-resident path): allocate/free on the context's device, copy. */
 int pfaai_device_alloc(pfaai_ctx* ctx, void** ptr, int64_t bytes);

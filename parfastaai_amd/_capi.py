@@ -30,7 +30,7 @@ FLAG_EMIT_JAC = 2
 EXPORTS = [
     "pfaai_version", "pfaai_create", "pfaai_destroy", "pfaai_last_error", "pfaai_load",
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
-    "pfaai_debug_row_counts", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
+    "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing",
 ]
 
@@ -77,6 +77,7 @@ def load_library():
         "pfaai_compute": (ctypes.c_int, [vp, u32, vp, vp, vp]),
         "pfaai_last_stats": (ctypes.c_int, [vp, P64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "pfaai_debug_row_counts": (ctypes.c_int, [vp, i64, vp]),
+        "pfaai_debug_div_check": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
         "pfaai_device_alloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), i64]),
         "pfaai_device_free": (ctypes.c_int, [vp, vp]),
         "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
@@ -180,6 +181,12 @@ class Engine:
         self._check(self.lib.pfaai_timing(self.ctx, int(reset), ctypes.byref(n), ctypes.byref(b), ctypes.byref(r)),
                     "pfaai_timing")
         return n.value, b.value, r.value
+
+    def debug_div_check(self, c_max, d_max):
+        """Mismatches of the kernels' exact small-integer division vs IEEE '/'."""
+        n = ctypes.c_int64()
+        self._check(self.lib.pfaai_debug_div_check(self.ctx, c_max, d_max, ctypes.byref(n)), "pfaai_debug_div_check")
+        return n.value
 
     def debug_row_counts(self, row, n_prot, n_ids):
         out = np.zeros((n_prot, n_ids), dtype=np.int32)

@@ -71,7 +71,7 @@ struct pfaai_ctx {
 
 namespace {
 
-constexpr int kDefaultRowsVariant = 11;  // fused genome-major k_rows (fastest measured: 19.3 ms at 10k)
+constexpr int kDefaultRowsVariant = 18;  // k_rows_pl, 4-lane groups x 16-B member loads (fastest measured: 16.8 ms at 10k)
 constexpr int64_t kPlMaxGlen = kRowThreads;
 constexpr size_t P_SLAB_MAX = (size_t)3 << 30;  // bytes of one protein's count slab (< 4 GiB)  // k_rows_pl: G list entries per (genome, protein)
 
@@ -321,7 +321,34 @@ void launch_rows_pl_kw(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, dou
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
     const size_t lds = (2 * (size_t)KW * kRowThreads + c->prob.n_prot + 1) * sizeof(uint32_t);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    if (c->occupancy == 14)
+    if (c->occupancy == 16)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 23)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, false, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads),
+                           lds, s, c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 24)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, false, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads),
+                           lds, s, c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 21)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s,
+                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 22)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s,
+                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 19)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
+                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 20)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
+                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 18)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 17)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 3, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else if (c->occupancy == 14)
         hipLaunchKernelGGL((k_rows_pl<MODE, KW, 16>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     else if (c->occupancy == 15)
@@ -410,7 +437,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         (void)launch_rows_2p<MODE>(c, rb, re, flags, aji, S, N, s);
         return;
     }
-    if (c->occupancy == 12 || c->occupancy == 14 || c->occupancy == 15) {
+    if (c->occupancy == 12 || c->occupancy >= 14) {
         launch_rows_pl<MODE>(c, rb, re, flags, aji, S, N, s);
         return;
     }
@@ -783,7 +810,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     {
         const char* occ = getenv("PFAAI_ROWS_OCC");
         const int v = occ ? atoi(occ) : 0;
-        c->occupancy = (v >= 1 && v <= 15) ? v : kDefaultRowsVariant;
+        c->occupancy = (v >= 1 && v <= 24) ? v : kDefaultRowsVariant;
         if ((c->occupancy == 12 || c->occupancy >= 14) && c->max_glen > kPlMaxGlen) c->occupancy = 11;  // lists too long to pipeline
         if (c->occupancy == 13 && !c->has_g) c->occupancy = 3;
         const char* bud = getenv("PFAAI_COUNT_BUDGET_MB");  // count-tensor budget of the two-phase path
@@ -915,6 +942,41 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h_counts, out, cells * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_OK;
+}
+
+}  // extern "C"
+
+namespace {
+__global__ void k_div_check(int32_t c_max, int32_t d_max, unsigned long long* bad) {
+    const int32_t c = 1 + (int32_t)blockIdx.y;  // c <= c_max by the grid
+    unsigned long long nb = 0;
+    for (int64_t d = c + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d <= d_max; d += (int64_t)gridDim.x * blockDim.x) {
+        const double q0 = (double)c / (double)d;
+        const double q1 = exact_div_small((double)c, (double)d);
+        nb += __double_as_longlong(q0) != __double_as_longlong(q1);
+    }
+    if (nb) atomicAdd(bad, nb);
+    (void)c_max;
+}
+}  // namespace
+
+extern "C" {
+
+int pfaai_debug_div_check(pfaai_ctx* c, int32_t c_max, int32_t d_max, int64_t* mismatches) {
+    if (!c || !mismatches || c_max < 1 || d_max < c_max || d_max >= (1 << 24) || c_max > 65535)
+        return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->dbg, sizeof(unsigned long long));
+    if (rc) return rc;
+    auto* bad = static_cast<unsigned long long*>(c->dbg.p);
+    HIPCHK(c, hipMemsetAsync(bad, 0, sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(k_div_check, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
+    HIPCHK(c, hipGetLastError());
+    unsigned long long h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *mismatches = (int64_t)h;
     return PFAAI_OK;
 }
 

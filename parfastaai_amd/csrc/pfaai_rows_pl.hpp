@@ -35,6 +35,8 @@
 // genome-major input, every (genome, protein) G list <= 1024 entries,
 // ncw <= KW*1024 counter words per chunk.
 #pragma once
+#include <type_traits>
+
 #include "pfaai_counts.hpp"  // buffer-load helpers
 
 namespace pfaai {
@@ -93,6 +95,38 @@ __device__ __forceinline__ void pl_scatter(const Dev& d, int32_t a, int32_t b, u
     ++ev;
 }
 
+// Branch-free E triple: every lane issues its ds_add_u32; a lane without a
+// valid member adds 0 to a counter word of its own (lane-private address, so
+// no same-address serialisation).  Exec-mask branches cost more than the
+// LDS op they would skip (SQ_INSTS_SALU/BRANCH dominated the branchy form).
+template <int MODE>
+__device__ __forceinline__ void bf_scatter(const Dev& d, int32_t a, int32_t b, bool ok, uint32_t* acc, int32_t cc0,
+                                           int32_t wlo, int32_t whi, uint32_t& ev) {
+    ok = ok && b >= wlo && b < whi;
+    if (MODE == 1) ok = ok && b != a && (!d.is_q[ok ? b : a] || b > a);  // isValidPair, ds_impl.hpp:270-273
+    const uint32_t o = ok ? (uint32_t)(b - cc0) : (uint32_t)(threadIdx.x & 63) << 1;
+    atomicAdd(&acc[o >> 1], (uint32_t)ok << ((o & 1u) << 4));
+    ev += ok;
+}
+
+// c / d for integers 1 <= c <= d < 2^24, bit-identical to IEEE division:
+// the same reciprocal, Newton steps and final residual correction that the
+// compiler expands '/' into (v_rcp_f64, 2 x fma refinement, mul, fma
+// residual, fma correction), minus v_div_scale / v_div_fmas / v_div_fixup,
+// which are the identity for operands this far from the exponent limits
+// (no scaling needed, no inf/nan/zero/denormal cases).  Exhaustively
+// checked against '/' on the GPU (tests/test_gpu_div.py).
+__device__ __forceinline__ double exact_div_small(double c, double dd) {
+    double y = __builtin_amdgcn_rcp(dd);
+    double e = __builtin_fma(-dd, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-dd, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = c * y;
+    const double r = __builtin_fma(-dd, q, c);
+    return __builtin_fma(r, y, q);
+}
+
 // Member loads of the line tasks k0 + u*64 (u < U) of this lane's
 // 16-lane group: task ids and run ranges are read from LDS in batches of 4
 // (all reads of a batch in flight together), then every lane issues its
@@ -121,6 +155,33 @@ __device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, cons
     return ok_mask;
 }
 
+// 4-lane-group form: a lane loads 4 consecutive members (16 B) of its
+// group's line task k0 + u*256, so one wave instruction covers 16 lines.
+// Bits 4u..4u+3 of the returned mask: b[u].{x,y,z,w} are members.
+template <int U>
+__device__ __forceinline__ uint32_t pl_issue4(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k0, int rem,
+                                              int gl4, uint4* b) {
+    constexpr int NG = kRowThreads / 4;
+    uint32_t ok_mask = 0u;
+    uint32_t t[U];
+    uint2 rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = tk[min(k0 + u * NG, kPlTaskCap - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) rr[u] = rt[t[u] & 1023u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t m0 = (rr[u].x & ~(uint32_t)(kGroup - 1)) + (t[u] >> 10) * kGroup + 4u * (uint32_t)gl4;
+        const bool task = u * NG < rem && t[u] != kPlNoTask;
+        uint32_t ok4 = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ok4 |= (uint32_t)(task && m0 + j >= rr[u].x && m0 + j < rr[u].y) << j;
+        ok_mask |= ok4 << (4 * u);
+        b[u] = bld_u128(fg, ok4 ? m0 * 4u : 0xFFFFFFF0u, 0u);
+    }
+    return ok_mask;
+}
+
 // Diagnostics (flags 0x1000): per-stage clock accumulation, written by wave
 // 0 of each workgroup into s_out as 8 doubles per workgroup.
 #define PL_TICK(slot)                                   \
@@ -130,7 +191,7 @@ __device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, cons
         tlast = t_;                                     \
     }
 
-template <int MODE, int KW, int U>
+template <int MODE, int KW, int U, int GL = kGroup, bool DEEP = false, bool BAL = false, bool BF = false>
 __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
     Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags, const unsigned long long* __restrict__ first_key,
     double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
@@ -143,7 +204,8 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
     __shared__ uint32_t ntask[3], nwhole[3];   // by protein % 3
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int grp = tid / kGroup, gl = tid % kGroup;
+    const int grp = tid / GL, gl = tid % GL;
+    constexpr int NG = kRowThreads / GL;  // lane groups
     const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
@@ -188,12 +250,15 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
     // Both return the raw load: nothing may touch a prefetched value before
     // its consumer, or the compiler waits for it on the spot.
     auto glen = [&](int p) -> uint32_t { return p < P ? uni(goff[p + 1]) - uni(goff[p]) : 0u; };
+    // BAL: G entry e of a protein goes to wave e % 16, lane e / 16, so every
+    // wave cuts about 1/16 of the runs (instead of the first few waves all)
+    const uint32_t ent = BAL ? (uint32_t)((tid & 63) * (kRowThreads / 64) + (tid >> 6)) : (uint32_t)tid;
     auto s1 = [&](int p) -> int32_t {
         const uint32_t o = p < P ? uni(goff[p]) : 0u;
-        return (int32_t)bld_u32(r_g, (uint32_t)tid < glen(p) ? (uint32_t)tid * 4u : 0xFFFFFFF0u, o * 4u);
+        return (int32_t)bld_u32(r_g, ent < glen(p) ? ent * 4u : 0xFFFFFFF0u, o * 4u);
     };
     auto s2 = [&](int p, int32_t t) -> uint4 {
-        const bool ok = (uint32_t)tid < glen(p);
+        const bool ok = ent < glen(p);
         return bld_u128(r_blk, ok ? (uint32_t)t * 16u : 0xFFFFFFF0u, (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
     };
     // S3: line tasks of protein q from this thread's run (slot tid)
@@ -201,7 +266,7 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
         const int st = q & 1, cs = q % 3;
         uint2 r;
         const uint32_t nl = pl_prune(r4, wlo, whi, r);
-        rt[st][tid] = r;
+        rt[st][ent] = r;
         bool whole = nl > (uint32_t)kPlMaxLines;
         const uint32_t v = whole ? 0u : nl;
         const uint32_t inc = wave_incl_scan_dpp(v);
@@ -214,8 +279,16 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
         if (v) {
             const uint32_t e0 = base + inc - v;
             if (base + inc <= (uint32_t)kPlTaskCap) {
+                if constexpr (BAL) {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j)
+                        if (j < v) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
 #pragma unroll 1
-                for (uint32_t j = 0; j < v; ++j) tk[st][e0 + j] = (uint16_t)(tid | (j << 10));
+                    for (uint32_t j = 4; j < v; ++j) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
+                } else {
+#pragma unroll 1
+                    for (uint32_t j = 0; j < v; ++j) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
+                }
             } else {  // over capacity: the whole workgroup walks this run
                 for (uint32_t j = e0; j < (uint32_t)kPlTaskCap; ++j) tk[st][j] = kPlNoTask;
                 whole = true;
@@ -223,19 +296,38 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
         }
         const unsigned long long wb = __ballot(whole);
         if (wb) {
-            if (whole) atomicOr(&wmask[cs][tid >> 5], 1u << (tid & 31));
+            if (whole) atomicOr(&wmask[cs][ent >> 5], 1u << (ent & 31));
             if (lane == 0) atomicAdd(&nwhole[cs], (uint32_t)__popcll(wb));
         }
     };
 
     // prologue: runs of protein 0 cut into tasks; blk of protein 1; G of protein 2
+    // DEEP: G lists loaded 2 iterations before their run-table lookups, the
+    // run-table entries 2 iterations before their tasks are cut, T words one
+    // iteration before their normalisation (register rings).
     {
-        int32_t gt = s1(0);
-        uint4 r4 = s2(0, gt);
-        gt = s1(1);
-        s3(0, r4);
-        r4 = s2(1, gt);   // protein i+1 on loop entry
-        gt = s1(2);       // protein i+2 on loop entry
+        int32_t gt, gtB = -1;
+        uint4 r4, r4B = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t twp[KW];  // DEEP: T words of protein i-1
+        int32_t tap = 0;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) twp[k] = 0u;
+        if constexpr (DEEP) {
+            const int32_t g0_ = s1(0), g1_ = s1(1), g2_ = s1(2);
+            const uint4 r0_ = s2(0, g0_);
+            r4 = s2(1, g1_);   // protein i+1 on loop entry
+            r4B = s2(2, g2_);  // protein i+2
+            gt = s1(3);        // protein i+3
+            gtB = s1(4);       // protein i+4
+            s3(0, r0_);
+        } else {
+            gt = s1(0);
+            r4 = s2(0, gt);
+            gt = s1(1);
+            s3(0, r4);
+            r4 = s2(1, gt);   // protein i+1 on loop entry
+            gt = s1(2);       // protein i+2 on loop entry
+        }
         __syncthreads();
 
 #pragma unroll 1
@@ -246,7 +338,7 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
             const bool has_p = i >= 1 && uni(goff[i]) > uni(goff[i - 1]);
             // T words of protein i-1 (normalised below, after the member loads are in flight)
             uint32_t tw[KW];
-            const int pt = i >= 1 ? i - 1 : 0;
+            const int pt = DEEP ? min(i, P - 1) : (i >= 1 ? i - 1 : 0);  // DEEP: protein i, used next iteration
             const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
 #pragma unroll
             for (int k = 0; k < KW; ++k)
@@ -255,12 +347,15 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
             PL_TICK(0)
             // S4 (issue): first round of member loads of protein i
             const int nt = (has_i && !(flags & 0x400u)) ? min((int)uni(ntask[cs]), kPlTaskCap) : 0;  // 0x400: diagnostics, no member loads
-            int32_t b[U];
-            uint32_t okm = pl_issue<U>(r_fg, tk[st], rt[st], grp, nt - grp, gl, b);
+            using BT = typename std::conditional<GL == 4, uint4, int32_t>::type;
+            BT b[U];
+            uint32_t okm;
+            if constexpr (GL == 4) okm = pl_issue4<U>(r_fg, tk[st], rt[st], grp, nt - grp, gl, b);
+            else okm = pl_issue<U>(r_fg, tk[st], rt[st], grp, nt - grp, gl, b);
             PL_TICK(1)
             // prefetches S2, S1 (after the member loads: vmcnt retires in order)
-            const uint4 r4n = s2(i + 2, gt);
-            gt = s1(i + 3);
+            const uint4 r4n = DEEP ? s2(i + 3, gt) : s2(i + 2, gt);
+            const int32_t gtn = DEEP ? s1(i + 5) : s1(i + 3);
             PL_TICK(2)
             // S5: normalise protein i-1
             if (has_p && (flags & 0x100u)) {  // diagnostics: clear only
@@ -269,6 +364,25 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
                 for (int k = 0; k < KW; ++k) {
                     const int32_t w = tid + k * kRowThreads;
                     if (w < ncw) acc_p[w] = 0u;
+                }
+            } else if (has_p && BF) {
+                uint32_t* acc_p = acc + (st ^ 1) * W;
+                const int32_t tap_ = DEEP ? tap : ta;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) {
+                    if (k * kRowThreads + (tid & ~63) < ncw) {  // wave-uniform: the wave's words exist
+                        const int32_t w = tid + k * kRowThreads;
+                        const uint32_t v = acc_p[w];
+                        acc_p[w] = 0u;
+                        const uint32_t t2 = DEEP ? twp[k] : tw[k];
+                        const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+                        const int32_t d0 = max(tap_ + (int32_t)(t2 & 0xFFFFu) - c0, 1);
+                        const int32_t d1 = max(tap_ + (int32_t)(t2 >> 16) - c1, 1);
+                        // c = 0 adds +0.0: S is unchanged bit for bit
+                        S[2 * k] += exact_div_small((double)c0, (double)d0);
+                        S[2 * k + 1] += exact_div_small((double)c1, (double)d1);
+                        N[k] += (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 16);
+                    }
                 }
             } else if (has_p) {
                 uint32_t* acc_p = acc + (st ^ 1) * W;
@@ -281,11 +395,11 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
                             acc_p[w] = 0u;
                             const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                             if (c0) {
-                                S[2 * k] += (double)c0 / (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0);
+                                S[2 * k] += (double)c0 / (double)((DEEP ? tap : ta) + (int32_t)((DEEP ? twp[k] : tw[k]) & 0xFFFFu) - c0);
                                 N[k] += 1u;
                             }
                             if (c1) {
-                                S[2 * k + 1] += (double)c1 / (double)(ta + (int32_t)(tw[k] >> 16) - c1);
+                                S[2 * k + 1] += (double)c1 / (double)((DEEP ? tap : ta) + (int32_t)((DEEP ? twp[k] : tw[k]) >> 16) - c1);
                                 N[k] += 1u << 16;
                             }
                         }
@@ -295,14 +409,36 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
             PL_TICK(3)
             // S4 (complete): atomics, further rounds, whole-workgroup runs
             if (has_i) {
+                auto scat = [&]() {
+                    if constexpr (GL == 4 && BF) {
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    pl_scatter<MODE>(d, a, (okm >> u) & 1u ? b[u] : -1, acc_i, cc0, wlo, whi, ev, flags);
-                for (int k0 = grp + U * kNumGroups; k0 < nt; k0 += U * kNumGroups) {
-                    okm = pl_issue<U>(r_fg, tk[st], rt[st], k0, nt - k0, gl, b);
+                        for (int u = 0; u < U; ++u) {
+                            const uint32_t m = okm >> (4 * u);
+                            bf_scatter<MODE>(d, a, (int32_t)b[u].x, m & 1u, acc_i, cc0, wlo, whi, ev);
+                            bf_scatter<MODE>(d, a, (int32_t)b[u].y, m & 2u, acc_i, cc0, wlo, whi, ev);
+                            bf_scatter<MODE>(d, a, (int32_t)b[u].z, m & 4u, acc_i, cc0, wlo, whi, ev);
+                            bf_scatter<MODE>(d, a, (int32_t)b[u].w, m & 8u, acc_i, cc0, wlo, whi, ev);
+                        }
+                    } else if constexpr (GL == 4) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        pl_scatter<MODE>(d, a, (okm >> u) & 1u ? b[u] : -1, acc_i, cc0, wlo, whi, ev, flags);
+                        for (int u = 0; u < U; ++u) {
+                            const uint32_t m = okm >> (4 * u);
+                            pl_scatter<MODE>(d, a, (m & 1u) ? (int32_t)b[u].x : -1, acc_i, cc0, wlo, whi, ev, flags);
+                            pl_scatter<MODE>(d, a, (m & 2u) ? (int32_t)b[u].y : -1, acc_i, cc0, wlo, whi, ev, flags);
+                            pl_scatter<MODE>(d, a, (m & 4u) ? (int32_t)b[u].z : -1, acc_i, cc0, wlo, whi, ev, flags);
+                            pl_scatter<MODE>(d, a, (m & 8u) ? (int32_t)b[u].w : -1, acc_i, cc0, wlo, whi, ev, flags);
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            pl_scatter<MODE>(d, a, (okm >> u) & 1u ? b[u] : -1, acc_i, cc0, wlo, whi, ev, flags);
+                    }
+                };
+                scat();
+                for (int k0 = grp + U * NG; k0 < nt; k0 += U * NG) {
+                    if constexpr (GL == 4) okm = pl_issue4<U>(r_fg, tk[st], rt[st], k0, nt - k0, gl, b);
+                    else okm = pl_issue<U>(r_fg, tk[st], rt[st], k0, nt - k0, gl, b);
+                    scat();
                 }
                 if (uni(nwhole[cs])) {
                     for (int wd = 0; wd < kRowThreads / 32; ++wd) {
@@ -320,7 +456,18 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
             PL_TICK(4)
             // S3: tasks of protein i+1 (last: the member ids and T words are dead here)
             if (i + 1 < P && !(flags & 0x800u)) s3(i + 1, r4);  // 0x800: diagnostics, no tasks
-            r4 = r4n;
+            if constexpr (DEEP) {
+                r4 = r4B;
+                r4B = r4n;
+                gt = gtB;
+                gtB = gtn;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) twp[k] = tw[k];
+                tap = ta;
+            } else {
+                r4 = r4n;
+                gt = gtn;
+            }
             // recycle the protein-(i+2) counter set (last read by S4(i-1))
             if (tid < 32) wmask[(i + 2) % 3][tid] = 0u;
             if (tid == 32) { ntask[(i + 2) % 3] = 0u; nwhole[(i + 2) % 3] = 0u; }

@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--genomes", type=int, default=10000)
 ap.add_argument("--prot", type=int, default=100)
 ap.add_argument("--ablate", type=int, default=0)
+ap.add_argument("--variant", type=int, default=12)
 a = ap.parse_args()
 g = syn.generate(a.genomes, a.prot)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
@@ -31,7 +32,7 @@ n_rows, n_pairs = eng.shape()
 d = eng.alloc(n_pairs * 8)
 sbuf = eng.alloc(max(n_pairs * 8, n_rows * 8 * 8 * 4))
 nbuf = eng.alloc(n_pairs * 4)
-os.environ["PFAAI_ROWS_OCC"] = "12"
+os.environ["PFAAI_ROWS_OCC"] = str(a.variant)
 eng.run(0, n_rows, 0, d)  # warm
 os.environ["PFAAI_ABLATE"] = str(0x10 | a.ablate)
 eng.timing(reset=True)
