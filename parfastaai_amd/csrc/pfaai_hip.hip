@@ -2,7 +2,8 @@
 //
 // Owns one device per context: the problem (Lp, F, T, mode maps) stays
 // resident in HBM after pfaai_load(); pfaai_run() is stream-ordered device
-// work only (no host sync, no allocation): K-W work-list build, then K-S+J.
+// work only (no host sync, no allocation): the run table (k_blk) or, for
+// F-only input, the sorted work lists, then the row kernel (K-S+J).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,7 +16,6 @@
 #include "pfaai_hip.h"
 #include "pfaai_kernels.hpp"
 #include "pfaai_rows_pl.hpp"
-#include "pfaai_counts.hpp"
 
 using namespace pfaai;
 
@@ -42,12 +42,7 @@ struct pfaai_ctx {
     int32_t max_cols = 0;
 
     // device-resident problem
-    DevBuf T16, T16c;
-    // two-phase row path (variant 13): per-row cell bases of the count tensor
-    std::vector<unsigned long long> cbase_h;
-    DevBuf cbase, counts;
-    int32_t cnt_chunks = 1;
-    size_t cnt_budget = 0;
+    DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
     int64_t max_glen = 0;  // longest (genome, protein) G list
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
     bool has_g = false;
@@ -62,8 +57,7 @@ struct pfaai_ctx {
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool timed = false;
-    int occupancy = 2;  // k_rows variant (PFAAI_ROWS_OCC=1|2|3|4)
-    int recs_batch = 1;  // k_recs_g chains per lane (PFAAI_RECS_BATCH=1|8)
+    int rows_kernel = 0;  // RowsKernel of the current run
     // per-run event triples for pfaai_timing (pool reused after each reset)
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;
@@ -71,9 +65,13 @@ struct pfaai_ctx {
 
 namespace {
 
-constexpr int kDefaultRowsVariant = 18;  // k_rows_pl, 4-lane groups x 16-B member loads (fastest measured: 16.8 ms at 10k)
-constexpr int64_t kPlMaxGlen = kRowThreads;
-constexpr size_t P_SLAB_MAX = (size_t)3 << 30;  // bytes of one protein's count slab (< 4 GiB)  // k_rows_pl: G list entries per (genome, protein)
+// Row kernels.  PL (k_rows_pl, 1024 threads, <= 64 VGPRs so two workgroups
+// share a CU: 12.2 ms at 10k vs 15.6 at one per CU) is the default for
+// genome-major input; PL512 is its 512-thread form (13.9 ms); FUSED (k_rows<true>) takes
+// G lists longer than k_rows_pl does; WORKLIST (k_rows<false> over sorted
+// work lists) serves F-only input.  PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist
+// overrides the choice (A/B runs, tools/gpu/ab_rows.py; tests).
+enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
 
 // scalars buffer layout (u64 each)
 enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
@@ -196,41 +194,6 @@ int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool firs
     return PFAAI_OK;
 }
 
-// Work-list build from the genome-major view (no sort): run table, lengths,
-// scan, one binary search per entry.
-template <int MODE>
-int build_records_g(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool first_event) {
-    const int64_t P = c->prob.n_prot;
-    const int64_t K = (re - rb) * P;
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    int* err = reinterpret_cast<int*>(sc + SC_ERR);
-    auto* rowptr = static_cast<unsigned long long*>(c->rowptr.p);
-    auto* len = static_cast<uint32_t*>(c->lens.p);
-    HIPCHK(c, hipMemsetAsync(c->blk.p, 0, c->blk.bytes, s));
-    hipLaunchKernelGGL(k_blk, dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, err);
-    if (first_event) {  // lexicographically first E triple, all rows (row Z)
-        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
-                           (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
-                           static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
-    }
-    hipLaunchKernelGGL(k_glen, dim3(ceil_div(K, 256)), dim3(256), 0, s, c->dev, rb, K, len);
-    int rc = scan_u32(c, len, K, rowptr, s);
-    if (rc) return rc;
-    const size_t glds = 0;
-    if (c->recs_batch == 0 && MODE == 0)
-        hipLaunchKernelGGL((k_recs_g<MODE, 0>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
-                           static_cast<uint2*>(c->recs.p));
-    else if (c->recs_batch == 8)
-        hipLaunchKernelGGL((k_recs_g<MODE, 8>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
-                           static_cast<uint2*>(c->recs.p));
-    else
-        hipLaunchKernelGGL((k_recs_g<MODE, 1>), dim3(re - rb), dim3(kTetraThreads), glds, s, c->dev, rb, rowptr,
-                           static_cast<uint2*>(c->recs.p));
-    HIPCHK(c, hipGetLastError());
-    return PFAAI_OK;
-}
-
 // Fused genome-major path: only the run table (+ the first E triple for the
 // ref-compat zero-overlap quirk); k_rows walks the G lists itself.
 template <int MODE>
@@ -260,203 +223,81 @@ int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* ou
     return PFAAI_OK;
 }
 
-int pick_kw(int32_t max_cols) {
-    static const int kws[] = {1, 2, 3, 4, 5, 6, 8, 10};
-    const int64_t words = ceil_div(std::max<int32_t>(max_cols, 1), 2);
-    for (int kw : kws)
-        if (words <= (int64_t)kw * kRowThreads) return kw;
-    return 10;  // wider rows are split into column chunks
+// Counter words per thread: the smallest KW with KW * nt >= the widest row
+// (in u16 pairs); wider rows are cut into column chunks of 2 * KW * nt.
+template <int NT>
+int pick_kw(int32_t max_cols, int kw_max) {
+    const int64_t words = ceil_div((int64_t)std::max<int32_t>(max_cols, 1) + 1, 2);
+    for (int kw = 1; kw < kw_max; ++kw)
+        if (words <= (int64_t)kw * NT) return kw;
+    return kw_max;
+}
+
+template <int MODE, int KW, int NT, int WPE = 4>
+void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+               hipStream_t s) {
+    const int32_t chunk = 2 * KW * NT;
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev, rb, chunk,
+                       flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
 template <int MODE, int KW>
-void launch_rows_kw(pfaai_ctx* c, int64_t rb, int64_t re, int32_t chunk, int32_t nchunks, uint32_t flags,
-                    double* aji, double* S, int32_t* N, hipStream_t s) {
+void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                   hipStream_t s) {
+    const int32_t chunk = 2 * KW * kRowThreads;
+    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
     const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
     auto* recs = static_cast<const uint2*>(c->recs.p);
-    if (c->occupancy >= 9) {
-        if (!c->has_g) return;  // checked by run_mode
-        if (c->occupancy == 11)
-            hipLaunchKernelGGL((k_rows<MODE, KW, 11>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
-                               rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-        else if (c->occupancy == 9)
-            hipLaunchKernelGGL((k_rows<MODE, KW, 9>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                               rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-        else
-            hipLaunchKernelGGL((k_rows<MODE, KW, 10>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
-                               rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    } else if (c->occupancy == 2)
-        hipLaunchKernelGGL((k_rows<MODE, KW, 2>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 8)
-        hipLaunchKernelGGL((k_rows<MODE, KW, 8>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 7)
-        hipLaunchKernelGGL((k_rows<MODE, KW, 7>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 6)
-        hipLaunchKernelGGL((k_rows<MODE, KW, 6>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 5)
-        hipLaunchKernelGGL((k_rows4<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), 3 * lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 4)
-        hipLaunchKernelGGL((k_rows_pipe<MODE, KW>), dim3(re - rb, nchunks), dim3(kRowThreads), 2 * lds, s, c->dev,
-                           rb, rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 3)
-        hipLaunchKernelGGL((k_rows<MODE, KW, 3>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+    if (c->rows_kernel == RK_FUSED)
+        hipLaunchKernelGGL((k_rows<MODE, KW, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     else
-        hipLaunchKernelGGL((k_rows<MODE, KW, 1>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+        hipLaunchKernelGGL((k_rows<MODE, KW, false>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
-// k_rows_pl (variant 12): KW <= 5 counter words per thread, wider rows are
-// cut into chunks of 10 240 columns starting at even columns.
-template <int MODE, int KW>
-void launch_rows_pl_kw(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-                       hipStream_t s) {
-    const int32_t chunk = 2 * KW * kRowThreads;
-    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
-    const size_t lds = (2 * (size_t)KW * kRowThreads + c->prob.n_prot + 1) * sizeof(uint32_t);
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    if (c->occupancy == 16)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 23)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, false, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads),
-                           lds, s, c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 24)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, false, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads),
-                           lds, s, c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 21)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s,
-                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 22)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, false, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s,
-                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 19)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
-                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 20)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 2, 4, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev,
-                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 18)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 1, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 17)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 3, 4>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 14)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 16>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else if (c->occupancy == 15)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 12>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, 8>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-}
-
 template <int MODE>
-void launch_rows_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-                    hipStream_t s) {
-    const int64_t words = ceil_div((int64_t)c->max_cols + 1, 2);
-    if (words <= 1 * kRowThreads) launch_rows_pl_kw<MODE, 1>(c, rb, re, flags, aji, S, N, s);
-    else if (words <= 2 * kRowThreads) launch_rows_pl_kw<MODE, 2>(c, rb, re, flags, aji, S, N, s);
-    else if (words <= 3 * kRowThreads) launch_rows_pl_kw<MODE, 3>(c, rb, re, flags, aji, S, N, s);
-    else if (words <= 4 * kRowThreads) launch_rows_pl_kw<MODE, 4>(c, rb, re, flags, aji, S, N, s);
-    else launch_rows_pl_kw<MODE, 5>(c, rb, re, flags, aji, S, N, s);
+void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                 hipStream_t s) {
+#define PL_CASE(NT, K) \
+    case K: launch_pl<MODE, K, NT>(c, rb, re, flags, aji, S, N, s); break;
+#define KR_CASE(K) \
+    case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
+    if (c->rows_kernel == RK_PL) {
+        switch (pick_kw<1024>(c->max_cols, 5)) {
+            case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 4: launch_pl<MODE, 4, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            default: launch_pl<MODE, 5, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+        }
+    } else if (c->rows_kernel == RK_PL512) {
+        switch (pick_kw<512>(c->max_cols, 10)) {
+            PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
+            PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
+            default: break;
+        }
+    } else {
+        switch (pick_kw<kRowThreads>(c->max_cols, 10)) {
+            KR_CASE(1) KR_CASE(2) KR_CASE(3) KR_CASE(4) KR_CASE(5) KR_CASE(6) KR_CASE(8) KR_CASE(10)
+            case 7: launch_k_rows<MODE, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 9: launch_k_rows<MODE, 10>(c, rb, re, flags, aji, S, N, s); break;
+            default: break;
+        }
+    }
+#undef PL_CASE
+#undef KR_CASE
 }
 
-// Two-phase row path (variant 13): rows are cut into tiles whose count
-// tensor (P x cells x 2 B) fits the budget; per tile k_counts then k_norm.
-template <int MODE>
-int launch_rows_2p(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-                   hipStream_t s) {
-    const int64_t P = c->prob.n_prot;
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    const auto* cb = static_cast<const unsigned long long*>(c->cbase.p);
-    const auto& h = c->cbase_h;
-    int64_t t0 = rb;
-    while (t0 < re) {
-        // largest tile from t0 within the budget (at least one row)
-        int64_t t1 = t0 + 1;
-        {
-            int64_t lo = t0 + 1, hi = re;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) / 2;
-                if ((h[mid] - h[t0]) * 2 * (uint64_t)P <= c->cnt_budget) lo = mid; else hi = mid - 1;
-            }
-            t1 = lo;
-        }
-        const uint64_t cells = h[t1] - h[t0];
-        const uint64_t pitch = cells / 2;  // words per protein
-        int rc = ensure(c, c->counts, std::max<uint64_t>(pitch * P * 4, 16));
-        if (rc) return rc;
-        auto* cnt = static_cast<uint32_t*>(c->counts.p);
-        const int64_t rows = t1 - t0;
-        const int64_t groups = (rows + kCntRowGroup - 1) / kCntRowGroup;
-        const int64_t total = groups * kCntRowGroup * c->cnt_chunks * P;
-        const int64_t grid = ceil_div(total, kXcds) * kXcds;
-        unsigned long long* prof = nullptr;  // diagnostics: PFAAI_PROF_COUNTS=1 prints k_counts stage clocks
-        if (getenv("PFAAI_PROF_COUNTS")) {
-            if ((rc = ensure(c, c->dbg, 8 * sizeof(unsigned long long)))) return rc;
-            prof = static_cast<unsigned long long*>(c->dbg.p);
-            HIPCHK(c, hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s));
-        }
-        const char* abl = getenv("PFAAI_CNT_ABLATE");  // diagnostics: bit 0 no atomics, bit 1 no member loads
-        const uint32_t dbg = abl ? (uint32_t)atoi(abl) : 0u;
-        const char* pad = getenv("PFAAI_CNT_LDS_PAD");  // diagnostics: extra LDS per workgroup (KiB) -> occupancy
-        const size_t padb = pad ? (size_t)atoi(pad) << 10 : 0;
-        hipLaunchKernelGGL((k_counts<MODE>), dim3((unsigned)grid), dim3(kCntThreads), padb, s, c->dev, t0, (int32_t)rows,
-                           c->cnt_chunks, cb, (uint64_t)pitch, cnt, sc + SC_EVENTS, prof, dbg);
-        if (prof) {
-            unsigned long long h8[8];
-            HIPCHK(c, hipMemcpyAsync(h8, prof, sizeof(h8), hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            const char* nm[8] = {"setup", "G+blk", "tasks", "barrier1", "scatter", "whole", "barrier2", "store"};
-            double tot = 0;
-            for (int k = 0; k < 8; ++k) tot += (double)h8[k];
-            for (int k = 0; k < 8; ++k)
-                fprintf(stderr, "k_counts %-9s %6.1f %%  %.0f cyc/item-pass\n", nm[k], 100.0 * h8[k] / tot,
-                        (double)h8[k] / (double)total);
-        }
-        hipLaunchKernelGGL((k_norm<MODE>), dim3((unsigned)rows), dim3(kNormThreads), P * sizeof(int32_t), s, c->dev, t0,
-                           cb, (uint64_t)pitch, (const uint32_t*)cnt, flags, sc + SC_FIRST_KEY, aji, S, N);
-        t0 = t1;
-    }
-    return PFAAI_OK;
-}
-
-template <int MODE>
-void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S,
-                 int32_t* N, hipStream_t s) {
-    if (c->occupancy == 13) {
-        (void)launch_rows_2p<MODE>(c, rb, re, flags, aji, S, N, s);
-        return;
-    }
-    if (c->occupancy == 12 || c->occupancy >= 14) {
-        launch_rows_pl<MODE>(c, rb, re, flags, aji, S, N, s);
-        return;
-    }
-    const int kw = pick_kw(c->max_cols);
-    const int32_t chunk = 2 * kw * kRowThreads;
-    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
-    switch (kw) {
-#define KCASE(K) \
-    case K: launch_rows_kw<MODE, K>(c, rb, re, chunk, nchunks, flags, aji, S, N, s); break;
-        KCASE(1) KCASE(2) KCASE(3) KCASE(4) KCASE(5) KCASE(6) KCASE(8) KCASE(10)
-#undef KCASE
-        default: break;
-    }
-}
-
-// Work-list space for the sorted (F-only) and searched (G, variants <= 8)
-// paths, sized for all rows: ~36 B per F entry of the row genomes.  The
-// default genome-major path (fused k_rows) needs none of it, so it is
-// allocated at load only for F-only input and otherwise on first use.
+// Work-list space for the sorted (F-only) path, sized for all rows: ~36 B per
+// F entry of the row genomes.  The genome-major kernels need none of it, so
+// it is allocated at load only for F-only input (and on first use by
+// pfaai_debug_row_counts).
 int ensure_worklists(pfaai_ctx* c) {
     if (c->wl_ready) return PFAAI_OK;
     const auto& p = c->prob;
@@ -503,14 +344,12 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     c->ev1 = ev[1];
     c->ev2 = ev[2];
     HIPCHK(c, hipEventRecord(c->ev0, s));
-    const bool fused = c->has_g && c->occupancy >= 9;
-    if (!fused) {
+    const bool wl = c->rows_kernel == RK_WORKLIST;
+    if (wl) {
         const int rcw = ensure_worklists(c);
         if (rcw) return rcw;
     }
-    int rc = fused     ? build_runs_g<MODE>(c, s, compat)
-             : c->has_g ? build_records_g<MODE>(c, rb, re, s, compat)
-                        : build_records<MODE>(c, rb, re, s, compat);
+    int rc = wl ? build_records<MODE>(c, rb, re, s, compat) : build_runs_g<MODE>(c, s, compat);
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
@@ -552,7 +391,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     if (!c) return PFAAI_OK;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&c->T16, &c->T16c, &c->cbase, &c->counts, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
+    for (DevBuf* b : {&c->T16, &c->T16c, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
@@ -742,23 +581,6 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
             }
         }
     }
-    // count-tensor cell layout: row r covers columns [clo & ~7, chi) padded to 8 cells
-    {
-        c->cbase_h.assign(c->n_rows + 1, 0);
-        int64_t maxc = 0;
-        for (int64_t r = 0; r < c->n_rows; ++r) {
-            const int32_t g = c->row_genome_h[r];
-            int64_t lo, hi;
-            if (p.mode == PFAAI_MODE_ALL) { lo = g + 1; hi = ni; }
-            else if (p.mode == PFAAI_MODE_QSUB) { lo = 0; hi = ni; }
-            else { lo = 0; hi = p.n_tgt; }
-            const int64_t cells = hi > lo ? ((hi - (lo & ~7LL) + 7) & ~7LL) : 0;
-            maxc = std::max(maxc, cells);
-            c->cbase_h[r + 1] = c->cbase_h[r] + cells;
-        }
-        c->cnt_chunks = (int32_t)std::max<int64_t>(1, ceil_div(maxc, 2 * kCntChunkW));
-        if ((rc = upload(c, c->cbase, c->cbase_h.data(), c->cbase_h.size()))) return rc;
-    }
     HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
     c->wl_ready = false;
     if (!c->has_g && (rc = ensure_worklists(c))) return rc;
@@ -806,21 +628,20 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     if (!aji && !S && !N) return fail(c, PFAAI_ERR_INVALID, "no output");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-    // tuning knobs for A/B runs (tools/gpu/ab_rows.py); unset = defaults
+    // row kernel: default by input, PFAAI_ROWS_KERNEL overrides (A/B runs)
     {
-        const char* occ = getenv("PFAAI_ROWS_OCC");
-        const int v = occ ? atoi(occ) : 0;
-        c->occupancy = (v >= 1 && v <= 24) ? v : kDefaultRowsVariant;
-        if ((c->occupancy == 12 || c->occupancy >= 14) && c->max_glen > kPlMaxGlen) c->occupancy = 11;  // lists too long to pipeline
-        if (c->occupancy == 13 && !c->has_g) c->occupancy = 3;
-        const char* bud = getenv("PFAAI_COUNT_BUDGET_MB");  // count-tensor budget of the two-phase path
-        c->cnt_budget = (size_t)(bud ? atoll(bud) : 16384) << 20;
-        // a protein's slab is addressed with 32-bit offsets in k_norm
-        c->cnt_budget = std::min<size_t>(c->cnt_budget, (size_t)P_SLAB_MAX * (size_t)c->prob.n_prot);
-        if (c->occupancy >= 9 && !c->has_g) c->occupancy = 3;  // fused variants walk the G lists
-        const char* rbv = getenv("PFAAI_RECS_BATCH");
-        const int r = rbv ? atoi(rbv) : 1;
-        c->recs_batch = (r == 0 || r == 8) ? r : 1;
+        int k = !c->has_g ? RK_WORKLIST : c->max_glen > kPlEntries ? RK_FUSED : RK_PL;
+        if (const char* v = getenv("PFAAI_ROWS_KERNEL")) {
+            const std::string x(v);
+            if (x == "pl") k = RK_PL;
+            else if (x == "pl512") k = RK_PL512;
+            else if (x == "fused") k = RK_FUSED;
+            else if (x == "worklist") k = RK_WORKLIST;
+            else return fail(c, PFAAI_ERR_INVALID, "PFAAI_ROWS_KERNEL must be pl, pl512, fused or worklist");
+        }
+        if (!c->has_g && k != RK_WORKLIST) k = RK_WORKLIST;       // the others walk the G lists
+        if (c->max_glen > kPlEntries && k != RK_WORKLIST) k = RK_FUSED;  // lists too long
+        c->rows_kernel = k;
     }
     if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
@@ -921,20 +742,17 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
     auto* out = static_cast<int32_t*>(c->dbg.p);
     switch (p.mode) {
         case 0:
-            if ((rc = c->has_g ? build_records_g<0>(c, row, row + 1, c->stream, false)
-                               : build_records<0>(c, row, row + 1, c->stream, false)))
+            if ((rc = build_records<0>(c, row, row + 1, c->stream, false)))
                 return rc;
             hipLaunchKernelGGL(k_row_counts<0>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;
         case 1:
-            if ((rc = c->has_g ? build_records_g<1>(c, row, row + 1, c->stream, false)
-                               : build_records<1>(c, row, row + 1, c->stream, false)))
+            if ((rc = build_records<1>(c, row, row + 1, c->stream, false)))
                 return rc;
             hipLaunchKernelGGL(k_row_counts<1>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;
         default:
-            if ((rc = c->has_g ? build_records_g<2>(c, row, row + 1, c->stream, false)
-                               : build_records<2>(c, row, row + 1, c->stream, false)))
+            if ((rc = build_records<2>(c, row, row + 1, c->stream, false)))
                 return rc;
             hipLaunchKernelGGL(k_row_counts<2>, dim3(1, nchunks), dim3(kRowThreads), lds, c->stream, c->dev, row, rowptr, recs, chunk, out);
             break;

@@ -5,24 +5,29 @@
 // (psort.hpp:27-53, 86 % of its wall time) and walks the sorted runs
 // (algorithm_impl.hpp:123-277).  Here E is never built and nothing is sorted:
 //
-//   K-W  k_entries + k_rs_* + k_rowptr: one workgroup per tetramer block of
-//        F finds the (tetramer, protein) runs with a wavefront ballot +
-//        prefix count and turns every F entry whose genome is an output row
-//        into a "member range" [lo, hi) of its run (the genomes it pairs
-//        with), keyed by (row, protein); a hand-written stable LSD radix
-//        sort groups them per (row, protein) and rowptr marks the groups.
-//   K-S+J k_rows          one workgroup per output row (genome A): for each
-//        protein in ascending order, scatters +1 into an LDS row of packed
-//        u16 intersection counters for every member B of every range
-//        (= the E triples (p, A, B) of that row), then normalises the row
-//        J = c / (T[p][A] + T[p][B] - c) in fp64 into per-column register
-//        accumulators S, N -- the exact protein-ordered sum of
-//        algorithm_impl.hpp:240-275 -- and finally writes AJI = S / N
-//        (algorithm_impl.hpp:318) at the reference's JAC index.
+//   K-W   k_blk (genome-major input): the run table, (protein, tetramer) ->
+//         run of F; the row kernels walk each row genome's own G entries.
+//         F-only input: k_entries + k_rs_* + k_rowptr -- one workgroup per
+//         tetramer block of F finds the (tetramer, protein) runs with a
+//         wavefront ballot + prefix count and turns every F entry whose
+//         genome is an output row into a "member range" [lo, hi) of its run,
+//         keyed by (row, protein); a hand-written stable LSD radix sort
+//         groups them per (row, protein) and rowptr marks the groups.
+//   K-S+J k_rows_pl (pfaai_rows_pl.hpp, the default) and k_rows (here: the
+//         fallback for very long G lists, and the F-only form): one
+//         workgroup per output row (genome A); for each protein in ascending
+//         order, scatter +1 into an LDS row of packed u16 intersection
+//         counters for every member B of every run holding A (= the E
+//         triples (p, A, B) of that row), then normalise the row
+//         J = c / (T[p][A] + T[p][B] - c) in fp64 into per-column register
+//         accumulators S, N -- the exact protein-ordered sum of
+//         algorithm_impl.hpp:240-275 -- and finally write AJI = S / N
+//         (algorithm_impl.hpp:318) at the reference's JAC index.
 //
 // Integer counts are exact (integer LDS atomics); fp64 sums are built in
 // ascending protein order per pair, so results are bit-identical to the
-// reference.  No fast-math: divisions are IEEE (v_div_scale/fmas/fixup).
+// reference.  No fast-math: divisions are IEEE (or the bit-identical
+// exact_div_small of pfaai_util.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -275,21 +280,14 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 }
 
 // ---------------------------------------------------------------------------
-// K-W1g (genome-major input): run table + work lists without any sort.
+// K-W1g (genome-major input): the run table.
 //   k_blk:    one workgroup per tetramer block: run heads by wavefront ballot,
 //             blk[p * 160000 + t] = {start, end, splitters} of run (t, p)
 //             in F; the splitters are the genome ids at the run's 64-B line
 //             boundaries 1..3 (21 bits each, 0x1FFFFF past the end), which
-//             let a row skip whole lines outside its column window.
-//   k_glen:   work-list length of every (row, protein) = its G list length.
-//   k_recs_g: one workgroup per output row; each G entry (A, p, t) of the
-//             row looks up its run and becomes the member range of A in it:
-//               ALL  [pos(A)+1, end)   pos(A) by binary search of the run's
-//                                      sorted genome ids
-//               QSUB [start, end)      (filtered per member at scatter time)
-//               QT   [start, first query)
-//             written at rowptr[(row, p)] + its rank in the G list, so the
-//             lists come out grouped per (row, protein) with no atomics.
+//             let a row skip whole lines outside its column window.  The row
+//             kernels then walk each row genome's own G entries (A, p, t):
+//             the runs holding A, i.e. its E triples (ds_helper.hpp:270-357).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int* __restrict__ err) {
     __shared__ int32_t runs[kMaxRuns + 1];
@@ -340,107 +338,6 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int* __restrict__ 
                 make_uint4((uint32_t)rs, (uint32_t)re, (uint32_t)sp, (uint32_t)(sp >> 32));
         }
         __syncthreads();
-    }
-}
-
-__global__ void k_glen(Dev d, int64_t row_begin, int64_t n_keys, uint32_t* __restrict__ len) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
-    const int64_t r = row_begin + k / d.n_prot, p = k % d.n_prot;
-    const int64_t gp = (int64_t)d.row_genome[r] * d.n_prot + p;
-    len[k] = (uint32_t)(d.G_off[gp + 1] - d.G_off[gp]);
-}
-
-// Each thread walks kRecsBatch entries at once: their G, run-table and
-// binary-search loads are issued together (8 independent chains in flight
-// per lane) -- the kernel is bound by dependent-load latency otherwise.
-// kRecsBatch = 0: ALL mode only, no search -- the record is the whole run;
-// members B <= A are dropped by the row's column window (cc0 = A + 1).
-template <int MODE, int kRecsBatchT>
-__global__ __launch_bounds__(kTetraThreads) void k_recs_g(Dev d, int64_t row_begin,
-                                                          const unsigned long long* __restrict__ rowptr,
-                                                          uint2* __restrict__ recs) {
-    // static 32 KiB on purpose: it caps k_recs_g at 5 workgroups per CU, which
-    // measured faster (11.3 ms vs 16.8 ms at 10k) than full occupancy -- the
-    // run searches thrash L2 with more rows in flight
-    __shared__ long long goff[kMaxRuns + 1];
-    const int tid = threadIdx.x;
-    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
-    const int32_t a = d.row_genome[row_begin + rl];
-    const int P = d.n_prot;
-    const int64_t g0 = (int64_t)a * P;
-    for (int p = tid; p <= P; p += kTetraThreads) goff[p] = d.G_off[g0 + p];
-    __syncthreads();
-    constexpr int kRecsBatch = kRecsBatchT > 0 ? kRecsBatchT : 1;
-    const int64_t k0 = goff[0], k1 = goff[P];
-    for (int64_t kb = k0 + tid; kb < k1; kb += (int64_t)kTetraThreads * kRecsBatch) {
-        int pr[kRecsBatch];
-        uint32_t lo[kRecsBatch], hi[kRecsBatch], end[kRecsBatch];
-        bool live[kRecsBatch];
-#pragma unroll
-        for (int u = 0; u < kRecsBatch; ++u) {
-            const int64_t k = kb + (int64_t)u * kTetraThreads;
-            live[u] = k < k1;
-            int plo = 0, phi = P;  // protein of entry k: last p with goff[p] <= k
-            while (phi - plo > 1) {
-                const int mid = (plo + phi) >> 1;
-                if (goff[mid] <= k) plo = mid; else phi = mid;
-            }
-            pr[u] = plo;
-        }
-        int32_t t[kRecsBatch];
-#pragma unroll
-        for (int u = 0; u < kRecsBatch; ++u) t[u] = live[u] ? d.G_tet[kb + (int64_t)u * kTetraThreads] : 0;
-#pragma unroll
-        for (int u = 0; u < kRecsBatch; ++u) {
-            const uint4 r4 = live[u] ? d.blk[(int64_t)pr[u] * kNTetramers + t[u]] : make_uint4(0u, 0u, 0u, 0u);
-            const uint2 run = make_uint2(r4.x, r4.y);
-            lo[u] = run.x;
-            hi[u] = run.y;
-            end[u] = run.y;
-            live[u] = live[u] && run.y > run.x;
-        }
-        if constexpr (MODE != 1 && kRecsBatchT > 0) {
-            // lockstep lower_bound of A (ALL) or of n_tgt (QT) in each run's sorted genome ids
-            const int32_t key = MODE == 0 ? a : d.n_tgt;
-            bool any = true;
-            while (any) {
-                any = false;
-                int32_t v[kRecsBatch];
-                uint32_t mid[kRecsBatch];
-#pragma unroll
-                for (int u = 0; u < kRecsBatch; ++u) {
-                    mid[u] = (lo[u] + hi[u]) >> 1;
-                    v[u] = (live[u] && lo[u] < hi[u]) ? d.Fg[mid[u]] : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < kRecsBatch; ++u) {
-                    if (live[u] && lo[u] < hi[u]) {
-                        if (v[u] < key) lo[u] = mid[u] + 1; else hi[u] = mid[u];
-                        any |= lo[u] < hi[u];
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kRecsBatch; ++u) {
-            const int64_t k = kb + (int64_t)u * kTetraThreads;
-            if (k >= k1) continue;
-            uint2 rec = make_uint2(0u, 0u);
-            if (live[u]) {
-                if constexpr (MODE == 0 && kRecsBatchT == 0) {
-                    rec = make_uint2(lo[u], end[u]);  // whole run: B <= A fall outside the column window
-                } else if constexpr (MODE == 0) {
-                    if (lo[u] < end[u] && d.Fg[lo[u]] == a) rec = make_uint2(lo[u] + 1u, end[u]);
-                } else if constexpr (MODE == 1) {
-                    rec = make_uint2(lo[u], end[u]);
-                } else {
-                    const uint4 run = d.blk[(int64_t)pr[u] * kNTetramers + t[u]];
-                    rec = make_uint2(run.x, lo[u]);
-                }
-            }
-            recs[rowptr[rl * P + pr[u]] + (k - goff[pr[u]])] = rec;
-        }
     }
 }
 
@@ -733,7 +630,7 @@ __device__ __forceinline__ uint32_t scatter_row_protein(const Dev& d, int32_t a,
 }
 
 // ---------------------------------------------------------------------------
-// Fused genome-major scatter (k_rows OCC 9): no work list at all.  The rows'
+// Fused genome-major scatter (k_rows<FUSED>): no work list at all.  The rows'
 // (row, protein) member ranges are exactly the runs (t, p) of the row
 // genome's own G entries (A, p, t) -- A is a member of each -- and the order
 // of ranges inside one protein does not matter to the integer counts.  So per
@@ -834,10 +731,6 @@ __device__ __forceinline__ uint32_t scatter_row_g(const Dev& d, int32_t a, int p
     return ev;
 }
 
-template <int MODE, int kUnroll>
-__device__ __forceinline__ uint32_t scatter_row_rle(const Dev& d, int32_t a, const uint2* __restrict__ recs,
-                                                    uint64_t rb, uint64_t re, uint32_t* acc, uint2* rec_lds,
-                                                    int32_t cc0, int32_t cc1);
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -850,23 +743,22 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // counter words w = t + k*1024 (k < KW), i.e. columns cc0+2w, cc0+2w+1, and
 // keeps their S (fp64) and N (packed u16) in registers across all proteins.
 // ---------------------------------------------------------------------------
-// OCC = 2: two workgroups per CU (<= 64 VGPRs), 4 ranges in flight per group;
-// OCC = 1: one workgroup per CU, 8 ranges in flight per group;
-// OCC = 3: as 2, but long ranges are walked by their group alone.
-template <int MODE, int KW, int OCC>
-__global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
+// Two workgroups per CU (<= 64 VGPRs).  FUSED: the genome-major walk of
+// scatter_row_g (G lists + run table, no work list; the fallback of
+// k_rows_pl for G lists longer than it takes); otherwise the work-list walk
+// of scatter_row_protein (F-only input), long ranges walked by their group.
+template <int MODE, int KW, bool FUSED>
+__global__ __launch_bounds__(kRowThreads, 8) void k_rows(
     Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
     const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
     const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
     unsigned long long* __restrict__ n_events) {
-    extern __shared__ uint32_t acc[];  // KW*1024 counter words (+ OCC 7: a u16 T row of 2*KW*1024)
-    constexpr bool kFusedG = OCC == 9 || OCC == 10 || OCC == 11;  // genome-major fused scatter (no work list)
+    extern __shared__ uint32_t acc[];  // KW*1024 counter words
     __shared__ uint2 rec_lds[kRowThreads];
-    __shared__ uint2 long_lds[OCC == 7 || OCC == 6 || OCC == 3 || OCC == 8 ? 1 : kRowThreads];
-    __shared__ uint16_t task_lds[kFusedG ? kTaskCap : 1];
+    __shared__ uint2 long_lds[FUSED ? kRowThreads : 1];
+    __shared__ uint16_t task_lds[FUSED ? kTaskCap : 1];
     __shared__ uint32_t wsum[kRowThreads / 64];
     __shared__ int n_long;
-    uint16_t* trow = reinterpret_cast<uint16_t*>(acc + KW * kRowThreads);
     const int tid = threadIdx.x;
     const int64_t rl = xcd_row(blockIdx.x, gridDim.x);  // local row
     const int32_t a = d.row_genome[row_begin + rl];
@@ -890,7 +782,7 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
 
     for (int p = 0; p < P; ++p) {
         uint64_t rb, re;
-        if constexpr (kFusedG) {
+        if constexpr (FUSED) {
             rb = (uint64_t)d.G_off[(int64_t)a * P + p];
             re = (uint64_t)d.G_off[(int64_t)a * P + p + 1];
         } else {
@@ -898,20 +790,12 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
             re = rowptr[rl * P + p + 1];
         }
         if (rb == re) continue;  // uniform: no E triple (p, a, *)
-        if (OCC == 7) {  // stage this protein's T row (u16) for the chunk's columns; read after the barrier
-            const int32_t* Tq = d.T + (int64_t)p * d.t_cols;
-            for (int c = tid; c < cc1 - cc0; c += kRowThreads)
-                trow[c] = (uint16_t)Tq[compat ? d.tcol_col[cc0 + c] : cc0 + c];
-        }
         if (flags & 0x200u) {  // diagnostics: 0x200 skips the scatter
-        } else if constexpr (kFusedG) {
-            ev += scatter_row_g<MODE, OCC == 9 ? 4 : 8, OCC == 11>(d, a, p, (int64_t)rb, (int64_t)re, acc, rec_lds, task_lds,
-                                                         wsum, long_lds, cc0, cc1);
-        } else if (OCC == 6 || OCC == 7) {
-            ev += scatter_row_rle<MODE, 4>(d, a, recs, rb, re, acc, rec_lds, cc0, cc1);
+        } else if constexpr (FUSED) {
+            ev += scatter_row_g<MODE, 8, true>(d, a, p, (int64_t)rb, (int64_t)re, acc, rec_lds, task_lds, wsum, long_lds,
+                                               cc0, cc1);
         } else {
-            ev += scatter_row_protein<MODE, (OCC == 1 || OCC == 8) ? 8 : 4, OCC != 3 && OCC != 8>(
-                d, a, recs, rb, re, acc, rec_lds, long_lds, &n_long, cc0, cc1);
+            ev += scatter_row_protein<MODE, 4, false>(d, a, recs, rb, re, acc, rec_lds, long_lds, &n_long, cc0, cc1);
         }
         __syncthreads();
         if (flags & 0x100u) {  // diagnostics: 0x100 skips the normalisation (counters just cleared)
@@ -931,13 +815,12 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     const int32_t b0 = cc0 + 2 * w;
                     if (c0) {
-                        const int32_t tb = OCC == 7 ? (int32_t)trow[2 * w] : Tp[compat ? d.tcol_col[b0] : b0];
+                        const int32_t tb = Tp[compat ? d.tcol_col[b0] : b0];
                         S[2 * k] += (double)c0 / (double)(ta + tb - c0);
                         N[k] += 1u;
                     }
                     if (c1) {
-                        const int32_t tb = OCC == 7 ? (int32_t)trow[2 * w + 1]
-                                                    : Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
+                        const int32_t tb = Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
                         S[2 * k + 1] += (double)c1 / (double)(ta + tb - c1);
                         N[k] += 1u << 16;
                     }
@@ -974,462 +857,6 @@ __global__ __launch_bounds__(kRowThreads, OCC == 1 ? 4 : 8) void k_rows(
             if (aji) aji[idx] = n ? s / (double)n : 0.0;
             if (s_out) s_out[idx] = s;
             if (n_out) n_out[idx] = n;
-        }
-    }
-}
-
-// Scatter with per-lane run-length accumulation (k_rows OCC 6): lane l of a
-// 16-lane group sees member l of each of its ranges; consecutive ranges of
-// one (row, protein) list mostly hold the same genomes at the same offsets
-// (a clade), so the lane keeps (column, count) in registers and only issues
-// an LDS atomic when its column changes -- exact for any input, and it cuts
-// the same-address LDS atomics that dominate clade-structured data.
-template <int MODE>
-__device__ __forceinline__ void rle_push(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0, int32_t cc1,
-                                         int32_t& rcol, uint32_t& rcnt, uint32_t& ev) {
-    if (b < 0) return;
-    if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;
-    if (b < cc0 || b >= cc1) return;
-    ++ev;
-    if (b == rcol) {
-        ++rcnt;
-        return;
-    }
-    if (rcnt) {
-        const uint32_t o = (uint32_t)(rcol - cc0);
-        atomicAdd(&acc[o >> 1], rcnt << ((o & 1u) << 4));
-    }
-    rcol = b;
-    rcnt = 1;
-}
-
-template <int MODE, int kUnroll>
-__device__ __forceinline__ uint32_t scatter_row_rle(const Dev& d, int32_t a, const uint2* __restrict__ recs,
-                                                    uint64_t rb, uint64_t re, uint32_t* acc, uint2* rec_lds,
-                                                    int32_t cc0, int32_t cc1) {
-    const int tid = threadIdx.x;
-    const int grp = tid / kGroup, gl = tid % kGroup;
-    uint32_t ev = 0;
-    int32_t rcol = -1;
-    uint32_t rcnt = 0;
-    for (uint64_t base = rb; base < re; base += kRowThreads) {  // uniform trip count
-        const int n = (int)((re - base) < (uint64_t)kRowThreads ? (re - base) : (uint64_t)kRowThreads);
-        __syncthreads();
-        if (tid < n) rec_lds[tid] = recs[base + tid];
-        __syncthreads();
-        for (int j = grp; j < n; j += kNumGroups * kUnroll) {
-            uint32_t lo[kUnroll], hi[kUnroll];
-            int32_t b[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int k = j + u * kNumGroups;
-                const uint2 r = k < n ? rec_lds[k] : make_uint2(0u, 0u);
-                lo[u] = r.x;
-                hi[u] = r.y;
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) b[u] = lo[u] + gl < hi[u] ? d.Fg[lo[u] + gl] : -1;
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) rle_push<MODE>(d, a, b[u], acc, cc0, cc1, rcol, rcnt, ev);
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-                for (uint32_t m = lo[u] + kGroup + gl; m < hi[u]; m += kGroup)
-                    scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
-        }
-    }
-    if (rcnt) {
-        const uint32_t o = (uint32_t)(rcol - cc0);
-        atomicAdd(&acc[o >> 1], rcnt << ((o & 1u) << 4));
-    }
-    return ev;
-}
-
-// ---------------------------------------------------------------------------
-// K-S+J, software-pipelined (k_rows_pipe): one barrier per protein.
-// Phase q overlaps three proteins:
-//   (1) the long-range tails of protein q-1 (whole workgroup; extra barrier
-//       only when there are any, i.e. runs longer than 64 after A),
-//   (2) prefetch of protein q+1's work list into registers,
-//   (3) the scatter of protein q into counter buffer q&1,
-//   (4) the normalisation of protein q-1 from buffer (q-1)&1 (S, N updated
-//       in ascending protein order, counters cleared),
-//   (5) the prefetched list stored into the other LDS stage buffer.
-// so the member-load latency of q hides behind the normalisation of q-1 and
-// the list load of q+1 behind both.
-// ---------------------------------------------------------------------------
-constexpr int kLongMax = 256;
-
-template <int MODE>
-__device__ __forceinline__ uint32_t scatter_pipe(const Dev& d, int32_t a, const uint2* stage,
-                                                 const uint2* __restrict__ recs, uint64_t rb, int n, uint32_t* acc,
-                                                 uint2* longq, int* nlong, int32_t cc0, int32_t cc1) {
-    const int tid = threadIdx.x;
-    const int grp = tid / kGroup, gl = tid % kGroup;
-    uint32_t ev = 0;
-    for (int j = grp; j < n; j += kNumGroups * 4) {
-        uint32_t lo[4], hi[4];
-        int32_t b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = j + u * kNumGroups;
-            const uint2 r = k < n ? (k < kRowThreads ? stage[k] : recs[rb + k]) : make_uint2(0u, 0u);
-            lo[u] = r.x;
-            hi[u] = r.y;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) b[u] = lo[u] + gl < hi[u] ? d.Fg[lo[u] + gl] : -1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) scatter_one<MODE>(d, a, b[u], acc, cc0, cc1, ev);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint32_t cut = hi[u] - lo[u] > kLongCut ? lo[u] + kLongCut : hi[u];
-            if (cut < hi[u]) {  // hand the tail to the whole workgroup (next phase)
-                int slot = 0;
-                if (gl == 0) slot = atomicAdd(nlong, 1);
-                slot = __shfl(slot, 0, kGroup);
-                if (slot < kLongMax) {
-                    if (gl == 0) longq[slot] = make_uint2(cut, hi[u]);
-                } else {
-                    cut = hi[u];  // queue full: the group walks it
-                }
-            }
-            for (uint32_t m = lo[u] + kGroup + gl; m < cut; m += kGroup)
-                scatter_one<MODE>(d, a, d.Fg[m], acc, cc0, cc1, ev);
-        }
-    }
-    return ev;
-}
-
-template <int KW>
-__device__ __forceinline__ void normalize_protein(const Dev& d, int p, int32_t tca, bool compat, uint32_t* acc,
-                                                  int32_t ncw, int32_t cc0, double* S, uint32_t* N) {
-    const int tid = threadIdx.x;
-    const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
-    const int32_t ta = Tp[tca];
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-        const int32_t w = tid + k * kRowThreads;
-        if (w < ncw) {
-            const uint32_t v = acc[w];
-            if (v) {
-                acc[w] = 0u;
-                const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                const int32_t b0 = cc0 + 2 * w;
-                if (c0) {
-                    const int32_t tb = Tp[compat ? d.tcol_col[b0] : b0];
-                    S[2 * k] += (double)c0 / (double)(ta + tb - c0);
-                    N[k] += 1u;
-                }
-                if (c1) {
-                    const int32_t tb = Tp[compat ? d.tcol_col[b0 + 1] : b0 + 1];
-                    S[2 * k + 1] += (double)c1 / (double)(ta + tb - c1);
-                    N[k] += 1u << 16;
-                }
-            }
-        }
-    }
-}
-
-template <int MODE, int KW>
-__global__ __launch_bounds__(kRowThreads, 8) void k_rows_pipe(
-    Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
-    const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
-    const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out,
-    int32_t* __restrict__ n_out, unsigned long long* __restrict__ n_events) {
-    extern __shared__ uint32_t acc2[];  // two counter rows of KW * 1024 words
-    __shared__ uint2 stage[2][kRowThreads];
-    __shared__ uint2 longq[2][kLongMax];
-    __shared__ int nlong[2];
-    const int tid = threadIdx.x;
-    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
-    const int32_t a = d.row_genome[row_begin + rl];
-    int32_t clo, chi;
-    row_cols<MODE>(d, a, clo, chi);
-    const int32_t cc0 = clo + (int32_t)blockIdx.y * chunk_cols;
-    const int32_t cc1 = min(chi, cc0 + chunk_cols);
-    if (cc0 >= cc1) return;  // uniform
-    const int32_t ncw = (cc1 - cc0 + 1) >> 1;
-    constexpr int32_t kStride = KW * kRowThreads;
-    const bool compat = flags & 1u;
-    const int P = d.n_prot;
-    const unsigned long long* rp = rowptr + rl * P;
-
-    for (int w = tid; w < ncw; w += kRowThreads) { acc2[w] = 0u; acc2[kStride + w] = 0u; }
-    if (tid < 2) nlong[tid] = 0;
-    double S[2 * KW];
-    uint32_t N[KW];
-#pragma unroll
-    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
-    const int32_t tca = compat ? d.tcol_row[a] : a;
-    uint32_t ev = 0;
-
-    uint64_t rb_cur = rp[0];
-    int n_cur = (int)(rp[1] - rb_cur);
-    if (tid < n_cur) stage[0][tid] = recs[rb_cur + tid];
-    int n_prev = 0;
-    __syncthreads();
-
-    for (int q = 0; q <= P; ++q) {
-        const int bq = q & 1;
-        uint32_t* acc_q = acc2 + bq * kStride;
-        uint32_t* acc_p = acc2 + (bq ^ 1) * kStride;
-        // (1) long tails of protein q-1
-        if (q >= 1) {
-            const int nl = min(nlong[bq ^ 1], kLongMax);
-            if (nl > 0) {
-                for (int i = 0; i < nl; ++i) {
-                    const uint2 r = longq[bq ^ 1][i];
-                    for (uint32_t m = r.x + tid; m < r.y; m += kRowThreads)
-                        scatter_one<MODE>(d, a, d.Fg[m], acc_p, cc0, cc1, ev);
-                }
-                __syncthreads();
-            }
-        }
-        // (2) prefetch protein q+1's list
-        uint64_t rb_next = 0;
-        int n_next = 0;
-        uint2 pre = make_uint2(0u, 0u);
-        if (q + 1 < P) {
-            rb_next = rp[q + 1];
-            n_next = (int)(rp[q + 2] - rb_next);
-            if (tid < n_next) pre = recs[rb_next + tid];
-        }
-        // (3) scatter protein q
-        if (q < P && n_cur > 0)
-            ev += scatter_pipe<MODE>(d, a, stage[bq], recs, rb_cur, n_cur, acc_q, longq[bq], &nlong[bq], cc0, cc1);
-        // (4) normalise protein q-1
-        if (q >= 1 && n_prev > 0) normalize_protein<KW>(d, q - 1, tca, compat, acc_p, ncw, cc0, S, N);
-        // (5) stage protein q+1
-        if (tid < n_next && tid < kRowThreads) stage[bq ^ 1][tid] = pre;
-        if (tid == 0) nlong[bq ^ 1] = 0;
-        n_prev = q < P ? n_cur : 0;
-        rb_cur = rb_next;
-        n_cur = n_next;
-        __syncthreads();
-    }
-
-    ev = wave_sum_u32(ev);
-    if ((tid & 63) == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-        const int32_t w = tid + k * kRowThreads;
-        if (w >= ncw) continue;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int32_t b = cc0 + 2 * w + h;
-            if (b >= cc1 || !col_valid<MODE>(d, a, b)) continue;
-            const int64_t idx = pair_index<MODE>(d, a, b, compat);
-            double s = S[2 * k + h];
-            int32_t n = (int32_t)((N[k] >> (16 * h)) & 0xFFFFu);
-            if (n == 0 && compat) {
-                const unsigned long long key = *first_key;
-                const int32_t p0 = key == ~0ull ? 0 : (int32_t)(key & ((1ull << 21) - 1));
-                const int32_t* Tp = d.T + (int64_t)p0 * d.t_cols;
-                s = 0.0 + 1.0 / (double)(Tp[tca] + Tp[d.tcol_col[b]] - 1);
-                n = 1;
-            }
-            if (aji) aji[idx] = n ? s / (double)n : 0.0;
-            if (s_out) s_out[idx] = s;
-            if (n_out) n_out[idx] = n;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K-S+J v4 (k_rows4): 4-lane groups with 16-byte loads, T row staged in LDS.
-//   * scatter: each group of 4 lanes owns one member range; lane l loads the
-//     int4 at (lo & ~3) + 4l, so one group covers 16 genome ids with one
-//     64-B request (one wave instruction = 16 ranges); members outside
-//     [lo, hi) are masked.  Two ranges per group are in flight.  Ranges
-//     longer than 64 members hand their tail to the whole workgroup.
-//   * per protein the T row of the chunk's columns is staged into LDS as u16
-//     (T < 2^16 is checked at load) while the previous protein is being
-//     normalised, so the normalisation reads no global memory.
-//   * phases: [normalise p-1 | stage list + T row of p] barrier [scatter p]
-//     barrier -- two barriers per protein (three when long tails exist).
-// ---------------------------------------------------------------------------
-constexpr int kG4 = 4;                        // lanes per range
-constexpr int kNumG4 = kRowThreads / kG4;     // 256 ranges per workgroup pass
-constexpr uint32_t kLongCut4 = 64;            // members a group walks before handing off
-
-template <int MODE>
-__device__ __forceinline__ void scatter4(const Dev& d, int32_t a, int4 v, uint32_t pos, uint32_t lo, uint32_t hi,
-                                         uint32_t* acc, int32_t cc0, int32_t cc1, uint32_t& ev) {
-    const int32_t e4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const uint32_t m = pos + e;
-        if (m >= lo && m < hi) scatter_one<MODE>(d, a, e4[e], acc, cc0, cc1, ev);
-    }
-}
-
-template <int MODE>
-__device__ __forceinline__ uint32_t scatter_row4(const Dev& d, int32_t a, const uint2* stage,
-                                                 const uint2* __restrict__ recs, uint64_t rb, int n, uint32_t* acc,
-                                                 uint2* longq, int* nlong, int32_t cc0, int32_t cc1) {
-    const int tid = threadIdx.x;
-    const int grp = tid / kG4, gl = tid % kG4;
-    const int4* F4 = reinterpret_cast<const int4*>(d.Fg);
-    uint32_t ev = 0;
-    for (int j = grp; j < n; j += kNumG4 * 2) {
-        uint32_t lo[2], hi[2], pos[2];
-        int4 v[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int k = j + u * kNumG4;
-            const uint2 r = k < n ? (k < kRowThreads ? stage[k] : recs[rb + k]) : make_uint2(0u, 0u);
-            lo[u] = r.x;
-            hi[u] = r.y;
-            pos[u] = (r.x & ~3u) + 4u * gl;
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) v[u] = pos[u] < hi[u] ? F4[pos[u] >> 2] : make_int4(-1, -1, -1, -1);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) scatter4<MODE>(d, a, v[u], pos[u], lo[u], hi[u], acc, cc0, cc1, ev);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t base = lo[u] & ~3u;
-            uint32_t cut = hi[u];
-            if (hi[u] > base + kLongCut4) {  // tail to the whole workgroup
-                cut = base + kLongCut4;
-                int slot = 0;
-                if (gl == 0) slot = atomicAdd(nlong, 1);
-                slot = __shfl(slot, 0, kG4);
-                if (slot < kLongMax) {
-                    if (gl == 0) longq[slot] = make_uint2(cut, hi[u]);
-                } else {
-                    cut = hi[u];  // queue full: the group walks it
-                }
-            }
-            for (uint32_t q = base + 16u + 4u * gl; q < cut; q += 16u)
-                scatter4<MODE>(d, a, F4[q >> 2], q, lo[u], cut, acc, cc0, cc1, ev);
-        }
-    }
-    return ev;
-}
-
-template <int MODE, int KW>
-__global__ __launch_bounds__(kRowThreads, 8) void k_rows4(
-    Dev d, int64_t row_begin, const unsigned long long* __restrict__ rowptr,
-    const uint2* __restrict__ recs, int32_t chunk_cols, uint32_t flags,
-    const unsigned long long* __restrict__ first_key, double* __restrict__ aji, double* __restrict__ s_out,
-    int32_t* __restrict__ n_out, unsigned long long* __restrict__ n_events) {
-    extern __shared__ uint32_t smem[];  // acc[KW*1024] words | T rows: 2 x (2*KW*1024) u16
-    __shared__ uint2 stage[kRowThreads];
-    __shared__ uint2 longq[kLongMax];
-    __shared__ int nlong;
-    __shared__ int32_t ta_s[2];
-    constexpr int32_t kWords = KW * kRowThreads;
-    uint32_t* acc = smem;
-    uint16_t* trow = reinterpret_cast<uint16_t*>(smem + kWords);  // [2][2 * kWords]
-    const int tid = threadIdx.x;
-    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
-    const int32_t a = d.row_genome[row_begin + rl];
-    int32_t clo, chi;
-    row_cols<MODE>(d, a, clo, chi);
-    const int32_t cc0 = clo + (int32_t)blockIdx.y * chunk_cols;
-    const int32_t cc1 = min(chi, cc0 + chunk_cols);
-    if (cc0 >= cc1) return;  // uniform
-    const int32_t ncols = cc1 - cc0, ncw = (ncols + 1) >> 1;
-    const bool compat = flags & 1u;
-    const int P = d.n_prot;
-    const unsigned long long* rp = rowptr + rl * P;
-    const int32_t tca = compat ? d.tcol_row[a] : a;
-
-    for (int w = tid; w < ncw; w += kRowThreads) acc[w] = 0u;
-    if (tid == 0) nlong = 0;
-    double S[2 * KW];
-    uint32_t N[KW];
-#pragma unroll
-    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
-    uint32_t ev = 0;
-    int n_prev = 0;
-    uint64_t rb = 0;
-    int n = 0;
-
-    for (int p = 0; p <= P; ++p) {
-        // ---- phase A: normalise p-1, stage p
-        if (p >= 1 && n_prev > 0) {
-            const uint16_t* tr = trow + ((p - 1) & 1) * (2 * kWords);
-            const int32_t ta = ta_s[(p - 1) & 1];
-#pragma unroll
-            for (int k = 0; k < KW; ++k) {
-                const int32_t w = tid + k * kRowThreads;
-                if (w < ncw) {
-                    const uint32_t v = acc[w];
-                    if (v) {
-                        acc[w] = 0u;
-                        const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                        if (c0) {
-                            S[2 * k] += (double)c0 / (double)(ta + (int32_t)tr[2 * w] - c0);
-                            N[k] += 1u;
-                        }
-                        if (c1) {
-                            S[2 * k + 1] += (double)c1 / (double)(ta + (int32_t)tr[2 * w + 1] - c1);
-                            N[k] += 1u << 16;
-                        }
-                    }
-                }
-            }
-        }
-        if (p < P) {
-            rb = rp[p];
-            n = (int)(rp[p + 1] - rb);
-            if (n > 0) {
-                if (tid < n) stage[tid] = recs[rb + tid];
-                const int32_t* Tp = d.T + (int64_t)p * d.t_cols;
-                uint16_t* tr = trow + (p & 1) * (2 * kWords);
-                for (int c = tid; c < ncols; c += kRowThreads)
-                    tr[c] = (uint16_t)Tp[compat ? d.tcol_col[cc0 + c] : cc0 + c];
-                if (tid == 0) ta_s[p & 1] = Tp[tca];
-            }
-        } else {
-            n = 0;
-        }
-        __syncthreads();
-        // ---- phase B: scatter p
-        if (n > 0 && !(flags & 0x200u)) {
-            ev += scatter_row4<MODE>(d, a, stage, recs, rb, n, acc, longq, &nlong, cc0, cc1);
-            __syncthreads();
-            const int nl = min(nlong, kLongMax);
-            if (nl > 0) {
-                const int4* F4 = reinterpret_cast<const int4*>(d.Fg);
-                for (int i = 0; i < nl; ++i) {
-                    const uint2 r = longq[i];  // r.x is 4-aligned
-                    for (uint32_t q = r.x + 4u * tid; q < r.y; q += 4u * kRowThreads)
-                        scatter4<MODE>(d, a, F4[q >> 2], q, r.x, r.y, acc, cc0, cc1, ev);
-                }
-                __syncthreads();
-                if (tid == 0) nlong = 0;
-            }
-        }
-        __syncthreads();
-        n_prev = n;
-    }
-
-    ev = wave_sum_u32(ev);
-    if ((tid & 63) == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-        const int32_t w = tid + k * kRowThreads;
-        if (w >= ncw) continue;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int32_t b = cc0 + 2 * w + h;
-            if (b >= cc1 || !col_valid<MODE>(d, a, b)) continue;
-            const int64_t idx = pair_index<MODE>(d, a, b, compat);
-            double s = S[2 * k + h];
-            int32_t nn = (int32_t)((N[k] >> (16 * h)) & 0xFFFFu);
-            if (nn == 0 && compat) {
-                const unsigned long long key = *first_key;
-                const int32_t p0 = key == ~0ull ? 0 : (int32_t)(key & ((1ull << 21) - 1));
-                const int32_t* Tp = d.T + (int64_t)p0 * d.t_cols;
-                s = 0.0 + 1.0 / (double)(Tp[tca] + Tp[d.tcol_col[b]] - 1);
-                nn = 1;
-            }
-            if (aji) aji[idx] = nn ? s / (double)nn : 0.0;
-            if (s_out) s_out[idx] = s;
-            if (n_out) n_out[idx] = nn;
         }
     }
 }

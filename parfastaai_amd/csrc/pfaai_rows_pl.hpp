@@ -1,5 +1,4 @@
-// pfaai_rows_pl.hpp -- k_rows_pl: the software-pipelined genome-major row
-// kernel (the default K-S+J of the fused path).
+// pfaai_rows_pl.hpp -- k_rows_pl: the default row kernel (genome-major input).
 //
 // What it computes is exactly k_rows (pfaai_kernels.hpp): for output row A
 // and every protein p in ascending order, the intersection counts
@@ -8,86 +7,55 @@
 // S += c / (T[p][A] + T[p][B] - c), N += 1 over c > 0
 // (algorithm_impl.hpp:240-275), then AJI = S / N (algorithm_impl.hpp:318).
 //
-// Why a new kernel: per protein, k_rows walks a chain of dependent global
-// loads (G list -> run table -> member ids -> LDS atomics -> barrier -> T ->
-// divide) and nothing else is in flight meanwhile; measured on MI355X it is
-// latency-serialised, not bandwidth- or LDS-bound.  Here the chain is cut
-// into five stages that run for five different proteins in the same
+// Per protein, a one-row workgroup walks a chain of dependent loads (G list
+// -> run table -> member ids -> LDS atomics -> barrier -> T -> divide).  The
+// chain is cut into stages that work on different proteins in the same
 // iteration, with ONE workgroup barrier per protein:
 //
-//   iteration i:  S1(i+3) load the row genome's G list for protein i+3
-//                 S2(i+2) load the run-table entries of protein i+2's list
+//   iteration i:  T(i-1)  T16 words of protein i-1 (for S5, loaded first)
+//                 S4a(i)  issue the member-id loads of protein i's line tasks
 //                 S3(i+1) cut protein i+1's runs into 16-member line tasks
 //                         (wave scan + one LDS atomic per wave, no barrier)
-//                 S4(i)   member-id loads + ds_add_u32 into counter row i&1
+//                 S2(i+2) issue the run-table lookups of protein i+2
+//                 S1(i+3) issue the G-list load of protein i+3
 //                 S5(i-1) normalise counter row (i-1)&1 into S, N; clear it
+//                 S4b(i)  ds_add_u32 the members into counter row i&1, then
+//                         any further task rounds and whole-workgroup runs
 //                 barrier
 //
-// Member-id loads of S4 are issued first, the prefetches of S1/S2 and the
-// T words of protein i after them (gfx9 vmcnt retires loads in order, so
-// waiting for the member ids never waits for a prefetch), and S3 + S5 run
-// while the member ids are in flight.  Two counter rows (u16 pairs) double
-// buffer S4 against S5.  Runs too long for line tasks, and tasks beyond the
-// LDS task capacity, are flagged in a per-protein bitmask and walked by the
-// whole workgroup in S4 -- slower, never wrong.
+// gfx9 retires vector loads in order (vmcnt), so the prefetches are issued
+// AFTER the member loads: waiting for the members never waits for them.
+// A line task is 16 members = 64 B; a 4-lane group takes one task and each
+// lane loads 4 members with one 16-B buffer load (a wave instruction covers
+// 16 lines), which measured 13 % faster than 16-lane groups of 4-B loads.
+// Two counter rows (packed u16 pairs) double-buffer S4 against S5.  Runs too
+// long for line tasks, and tasks beyond the LDS capacity, are flagged in a
+// per-protein bitmask and walked by the whole workgroup -- slower, never
+// wrong.
 //
-// Preconditions (checked on the host, pfaai_hip.hip pick_rows_kernel):
-// genome-major input, every (genome, protein) G list <= 1024 entries,
-// ncw <= KW*1024 counter words per chunk.
+// NT threads per workgroup and WPE waves per SIMD: the default is NT = 1024
+// with WPE = 8, i.e. <= 64 VGPRs (a few spilled at KW = 5) so that two
+// workgroups share a CU and one's barrier waits overlap the other's work
+// (12.2 ms at 10k vs 15.6 ms at one per CU); NT = 512 is the alternative
+// form (twice the counter words per thread).
+//
+// Preconditions (checked on the host, pfaai_hip.hip): genome-major input,
+// every (genome, protein) G list <= kPlEntries entries, ncw <= KW*NT
+// counter words per chunk, T < 2^16.
 #pragma once
-#include <type_traits>
-
-#include "pfaai_counts.hpp"  // buffer-load helpers
+#include "pfaai_util.hpp"
 
 namespace pfaai {
 
-constexpr int kPlTaskCap = 4096;   // u16 line tasks per protein stage
+constexpr int kPlEntries = 1024;   // G entries per (genome, protein) (host-checked)
+constexpr int kPlTaskCap = 4096;   // u16 line tasks per protein stage: run slot | line << 10
 constexpr int kPlMaxLines = 63;    // runs with more lines go to the whole-workgroup walk
 constexpr uint16_t kPlNoTask = 0xFFFFu;
-#ifndef PFAAI_PL_WAVES
-#define PFAAI_PL_WAVES 4  // waves per SIMD: one 1024-thread workgroup per CU (~85 VGPRs)
-#endif
 
-// Inclusive wave64 prefix sum with DPP row shifts and row broadcasts (no LDS).
-__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
-// 16-B blk entry -> member range [lo, hi) and line count after pruning to
-// the column window [wlo, whi) with the run's line splitters (k_blk).
-__device__ __forceinline__ uint32_t pl_prune(uint4 r4, int32_t wlo, int32_t whi, uint2& r) {
-    r = make_uint2(r4.x, r4.y);
-    if (r.y - r.x <= 1u) return 0u;  // a run of one member is A alone: no partner
-    const uint32_t first = r.x & ~(uint32_t)(kGroup - 1);
-    uint32_t nl = (r.y - first + kGroup - 1) / kGroup;
-    if (nl > 1u) {
-        const uint64_t sp = (uint64_t)r4.z | ((uint64_t)r4.w << 32);
-        uint32_t l0 = 0, l1 = nl;
-#pragma unroll
-        for (uint32_t i = 1; i <= (uint32_t)kSplitters; ++i) {
-            const int32_t f = (int32_t)((sp >> (kSplitBits * (i - 1))) & kSplitNone);
-            if (i < nl) {
-                if (f <= wlo) l0 = i;               // lines < i hold ids < f <= wlo
-                if (f >= whi && l1 > i) l1 = i;     // lines >= i hold ids >= f >= whi
-            }
-        }
-        if (l1 <= l0) return 0u;
-        if (l0) r.x = first + l0 * kGroup;
-        if (l1 < nl) r.y = first + l1 * kGroup;
-        nl = l1 - l0;
-    }
-    return nl;
-}
-
+// E triple (p, A, b): +1 into the u16 counter of column b.
 template <int MODE>
-__device__ __forceinline__ void pl_scatter(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0,
-                                           int32_t wlo, int32_t whi, uint32_t& ev, uint32_t flags = 0u) {
+__device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0, int32_t wlo,
+                                       int32_t whi, uint32_t& ev, uint32_t flags) {
     if (b < wlo || b >= whi) return;  // also drops b = -1 (no member)
     if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
     const uint32_t o = (uint32_t)(b - cc0);
@@ -95,117 +63,48 @@ __device__ __forceinline__ void pl_scatter(const Dev& d, int32_t a, int32_t b, u
     ++ev;
 }
 
-// Branch-free E triple: every lane issues its ds_add_u32; a lane without a
-// valid member adds 0 to a counter word of its own (lane-private address, so
-// no same-address serialisation).  Exec-mask branches cost more than the
-// LDS op they would skip (SQ_INSTS_SALU/BRANCH dominated the branchy form).
+// Member loads of line task k of this lane's 4-lane group: 4 members (16 B)
+// of the task's 64-B line, issued unconditionally (an out-of-range offset
+// where the lane has none).  Bit j of the result: member j of b is valid.
+__device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k, int nt, int gl,
+                                             uint4& b) {
+    const uint32_t t = tk[min(k, kPlTaskCap - 1)];
+    const uint2 rr = rt[t & 1023u];
+    const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + (t >> 10) * kGroup + 4u * (uint32_t)gl;
+    const bool task = k < nt && t != kPlNoTask;
+    uint32_t ok = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ok |= (uint32_t)(task && m0 + j >= rr.x && m0 + j < rr.y) << j;
+    b = bld_u128(fg, ok ? m0 * 4u : kOOB, 0u);
+    return ok;
+}
+
 template <int MODE>
-__device__ __forceinline__ void bf_scatter(const Dev& d, int32_t a, int32_t b, bool ok, uint32_t* acc, int32_t cc0,
-                                           int32_t wlo, int32_t whi, uint32_t& ev) {
-    ok = ok && b >= wlo && b < whi;
-    if (MODE == 1) ok = ok && b != a && (!d.is_q[ok ? b : a] || b > a);  // isValidPair, ds_impl.hpp:270-273
-    const uint32_t o = ok ? (uint32_t)(b - cc0) : (uint32_t)(threadIdx.x & 63) << 1;
-    atomicAdd(&acc[o >> 1], (uint32_t)ok << ((o & 1u) << 4));
-    ev += ok;
+__device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, uint32_t ok, uint32_t* acc, int32_t cc0,
+                                            int32_t wlo, int32_t whi, uint32_t& ev, uint32_t flags) {
+    pl_add<MODE>(d, a, (ok & 1u) ? (int32_t)b.x : -1, acc, cc0, wlo, whi, ev, flags);
+    pl_add<MODE>(d, a, (ok & 2u) ? (int32_t)b.y : -1, acc, cc0, wlo, whi, ev, flags);
+    pl_add<MODE>(d, a, (ok & 4u) ? (int32_t)b.z : -1, acc, cc0, wlo, whi, ev, flags);
+    pl_add<MODE>(d, a, (ok & 8u) ? (int32_t)b.w : -1, acc, cc0, wlo, whi, ev, flags);
 }
 
-// c / d for integers 1 <= c <= d < 2^24, bit-identical to IEEE division:
-// the same reciprocal, Newton steps and final residual correction that the
-// compiler expands '/' into (v_rcp_f64, 2 x fma refinement, mul, fma
-// residual, fma correction), minus v_div_scale / v_div_fmas / v_div_fixup,
-// which are the identity for operands this far from the exponent limits
-// (no scaling needed, no inf/nan/zero/denormal cases).  Exhaustively
-// checked against '/' on the GPU (tests/test_gpu_div.py).
-__device__ __forceinline__ double exact_div_small(double c, double dd) {
-    double y = __builtin_amdgcn_rcp(dd);
-    double e = __builtin_fma(-dd, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    e = __builtin_fma(-dd, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    const double q = c * y;
-    const double r = __builtin_fma(-dd, q, c);
-    return __builtin_fma(r, y, q);
-}
-
-// Member loads of the line tasks k0 + u*64 (u < U) of this lane's
-// 16-lane group: task ids and run ranges are read from LDS in batches of 4
-// (all reads of a batch in flight together), then every lane issues its
-// loads unconditionally (an out-of-range offset where it has no member, so
-// no exec-mask branches).  Bit u of the returned mask: b[u] is a member.
-template <int U>
-__device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k0, int rem,
-                                             int gl, int32_t* b) {
-    uint32_t ok_mask = 0u;
-#pragma unroll
-    for (int h = 0; h < U; h += 4) {
-        uint32_t t[4];
-        uint2 rr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = tk[min(k0 + (h + j) * kNumGroups, kPlTaskCap - 1)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rr[j] = rt[t[j] & 1023u];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t m = (rr[j].x & ~(uint32_t)(kGroup - 1)) + (t[j] >> 10) * kGroup + (uint32_t)gl;
-            const bool ok = (h + j) * kNumGroups < rem && t[j] != kPlNoTask && m >= rr[j].x && m < rr[j].y;
-            ok_mask |= (uint32_t)ok << (h + j);
-            b[h + j] = (int32_t)bld_u32(fg, ok ? m * 4u : 0xFFFFFFF0u, 0u);
-        }
-    }
-    return ok_mask;
-}
-
-// 4-lane-group form: a lane loads 4 consecutive members (16 B) of its
-// group's line task k0 + u*256, so one wave instruction covers 16 lines.
-// Bits 4u..4u+3 of the returned mask: b[u].{x,y,z,w} are members.
-template <int U>
-__device__ __forceinline__ uint32_t pl_issue4(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k0, int rem,
-                                              int gl4, uint4* b) {
-    constexpr int NG = kRowThreads / 4;
-    uint32_t ok_mask = 0u;
-    uint32_t t[U];
-    uint2 rr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) t[u] = tk[min(k0 + u * NG, kPlTaskCap - 1)];
-#pragma unroll
-    for (int u = 0; u < U; ++u) rr[u] = rt[t[u] & 1023u];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t m0 = (rr[u].x & ~(uint32_t)(kGroup - 1)) + (t[u] >> 10) * kGroup + 4u * (uint32_t)gl4;
-        const bool task = u * NG < rem && t[u] != kPlNoTask;
-        uint32_t ok4 = 0u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ok4 |= (uint32_t)(task && m0 + j >= rr[u].x && m0 + j < rr[u].y) << j;
-        ok_mask |= ok4 << (4 * u);
-        b[u] = bld_u128(fg, ok4 ? m0 * 4u : 0xFFFFFFF0u, 0u);
-    }
-    return ok_mask;
-}
-
-// Diagnostics (flags 0x1000): per-stage clock accumulation, written by wave
-// 0 of each workgroup into s_out as 8 doubles per workgroup.
-#define PL_TICK(slot)                                   \
-    if (prof) {                                         \
-        const uint64_t t_ = clock64();             \
-        tacc[slot] += t_ - tlast;                       \
-        tlast = t_;                                     \
-    }
-
-template <int MODE, int KW, int U, int GL = kGroup, bool DEEP = false, bool BAL = false, bool BF = false>
-__global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
-    Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags, const unsigned long long* __restrict__ first_key,
-    double* __restrict__ aji, double* __restrict__ s_out, int32_t* __restrict__ n_out,
-    unsigned long long* __restrict__ n_events) {
-    constexpr int W = KW * kRowThreads;        // counter words per row
-    extern __shared__ uint32_t pl_smem[];      // acc[2][W], goff[P + 1]
-    __shared__ uint2 rt[2][kRowThreads];       // runs of a protein stage: member range [lo, hi)
-    __shared__ uint16_t tk[2][kPlTaskCap];     // line tasks: run slot | line << 10
-    __shared__ uint32_t wmask[3][kRowThreads / 32];  // whole-workgroup runs, by protein % 3
-    __shared__ uint32_t ntask[3], nwhole[3];   // by protein % 3
+template <int MODE, int KW, int NT, int WPE = 4>
+__global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags,
+                                                   const unsigned long long* __restrict__ first_key,
+                                                   double* __restrict__ aji, double* __restrict__ s_out,
+                                                   int32_t* __restrict__ n_out,
+                                                   unsigned long long* __restrict__ n_events) {
+    constexpr int W = KW * NT;            // counter words per row chunk
+    constexpr int EPT = kPlEntries / NT;  // G entries per thread
+    constexpr int NG = NT / 4;            // 4-lane groups
+    extern __shared__ uint32_t pl_smem[];                // acc[2][W], goff[P + 1]
+    __shared__ uint2 rt[2][kPlEntries];                  // runs of a protein stage: member range [lo, hi)
+    __shared__ uint16_t tk[2][kPlTaskCap];               // line tasks
+    __shared__ uint32_t wmask[3][kPlEntries / 32];       // whole-workgroup runs, by protein % 3
+    __shared__ uint32_t ntask[3], nwhole[3];             // by protein % 3
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int grp = tid / GL, gl = tid % GL;
-    constexpr int NG = kRowThreads / GL;  // lane groups
+    const int grp = tid >> 2, gl = tid & 3;
     const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
@@ -221,270 +120,170 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
     uint32_t* goff = pl_smem + 2 * W;
 
     const int64_t g0 = d.G_off[(int64_t)a * P];
-    for (int p = tid; p <= P; p += kRowThreads) goff[p] = (uint32_t)(d.G_off[(int64_t)a * P + p] - g0);
-    for (int w = tid; w < 2 * W; w += kRowThreads) acc[w] = 0u;
+    for (int p = tid; p <= P; p += NT) goff[p] = (uint32_t)(d.G_off[(int64_t)a * P + p] - g0);
+    for (int w = tid; w < 2 * W; w += NT) acc[w] = 0u;
     if (tid < 3) { ntask[tid] = 0u; nwhole[tid] = 0u; }
-    if (tid < 3 * (kRowThreads / 32)) (&wmask[0][0])[tid] = 0u;
+    for (int w = tid; w < 3 * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
     const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
     const uint16_t* T16 = compat ? d.T16c : d.T16;
     const int64_t t16w = d.t16_cols >> 1;            // u32 words per protein row of T16
     double S[2 * KW];
-    uint32_t N[KW];
+    uint32_t N[KW];  // packed u16 pair counts
 #pragma unroll
     for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
     uint32_t ev = 0;
-    const bool prof = flags & 0x1000u;
-    uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tlast = prof ? clock64() : 0;
     __syncthreads();
 
     const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)d.n_f * 4u);
-    // LDS-sourced values that are uniform go through readfirstlane so buffer
-    // resources and scalar offsets stay in SGPRs (no waterfall loops)
-    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-    const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni(goff[P]) * 4u);
+    const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
     const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);
-    // S1: G list entry tid of protein p (a tetramer id; meaningful for tid < n(p))
-    // S2: run-table entry of that tetramer in protein p ({0,0,..} past the list)
-    // Both return the raw load: nothing may touch a prefetched value before
-    // its consumer, or the compiler waits for it on the spot.
-    auto glen = [&](int p) -> uint32_t { return p < P ? uni(goff[p + 1]) - uni(goff[p]) : 0u; };
-    // BAL: G entry e of a protein goes to wave e % 16, lane e / 16, so every
-    // wave cuts about 1/16 of the runs (instead of the first few waves all)
-    const uint32_t ent = BAL ? (uint32_t)((tid & 63) * (kRowThreads / 64) + (tid >> 6)) : (uint32_t)tid;
-    auto s1 = [&](int p) -> int32_t {
-        const uint32_t o = p < P ? uni(goff[p]) : 0u;
-        return (int32_t)bld_u32(r_g, ent < glen(p) ? ent * 4u : 0xFFFFFFF0u, o * 4u);
+    const rsrc_t r_t = mk_rsrc(d.T, (uint64_t)P * d.t_cols * 4u);
+    // S1 / S2 return the raw loads: nothing may touch a prefetched value
+    // before its consumer, or the compiler waits for it on the spot.
+    auto glen = [&](int p) -> uint32_t { return p < P ? uni_u32(goff[p + 1]) - uni_u32(goff[p]) : 0u; };
+    auto s1 = [&](int p, int32_t (&gt)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
+        const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const uint32_t e = (uint32_t)(tid + j * NT);
+            gt[j] = (int32_t)bld_u32(r_g, e < n ? e * 4u : kOOB, o * 4u);
+        }
     };
-    auto s2 = [&](int p, int32_t t) -> uint4 {
-        const bool ok = ent < glen(p);
-        return bld_u128(r_blk, ok ? (uint32_t)t * 16u : 0xFFFFFFF0u, (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+    auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT]) {  // run-table entries ({0..} past the list)
+        const uint32_t n = glen(p);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const uint32_t e = (uint32_t)(tid + j * NT);
+            r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB, (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+        }
     };
-    // S3: line tasks of protein q from this thread's run (slot tid)
-    auto s3 = [&](int q, uint4 r4) {
+    auto s3 = [&](int q, const uint4 (&r4)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
-        uint2 r;
-        const uint32_t nl = pl_prune(r4, wlo, whi, r);
-        rt[st][ent] = r;
-        bool whole = nl > (uint32_t)kPlMaxLines;
-        const uint32_t v = whole ? 0u : nl;
-        const uint32_t inc = wave_incl_scan_dpp(v);
-        const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
-        uint32_t base = 0;
-        if (tot) {  // wave-uniform
-            if (lane == 63) base = atomicAdd(&ntask[cs], tot);
-            base = (uint32_t)__shfl((int)base, 63, 64);
-        }
-        if (v) {
-            const uint32_t e0 = base + inc - v;
-            if (base + inc <= (uint32_t)kPlTaskCap) {
-                if constexpr (BAL) {
+        uint32_t nl[EPT], v = 0;
 #pragma unroll
-                    for (uint32_t j = 0; j < 4; ++j)
-                        if (j < v) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
-#pragma unroll 1
-                    for (uint32_t j = 4; j < v; ++j) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
-                } else {
-#pragma unroll 1
-                    for (uint32_t j = 0; j < v; ++j) tk[st][e0 + j] = (uint16_t)(ent | (j << 10));
-                }
-            } else {  // over capacity: the whole workgroup walks this run
-                for (uint32_t j = e0; j < (uint32_t)kPlTaskCap; ++j) tk[st][j] = kPlNoTask;
-                whole = true;
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * NT;
+            uint2 r;
+            nl[j] = run_lines(r4[j], wlo, whi, r);
+            rt[st][e] = r;
+            if (nl[j] > (uint32_t)kPlMaxLines) {
+                atomicOr(&wmask[cs][e >> 5], 1u << (e & 31));
+                atomicAdd(&nwhole[cs], 1u);
+                nl[j] = 0u;
             }
+            v += nl[j];
         }
-        const unsigned long long wb = __ballot(whole);
-        if (wb) {
-            if (whole) atomicOr(&wmask[cs][ent >> 5], 1u << (ent & 31));
-            if (lane == 0) atomicAdd(&nwhole[cs], (uint32_t)__popcll(wb));
+        // one LDS atomic per wave reserves the wave's tasks
+        const uint32_t inc = wave_scan_dpp(v);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        uint32_t base = 0;
+        if (tot) {
+            if (lane == 63) base = atomicAdd(&ntask[cs], tot);
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63);
+        }
+        uint32_t e0 = base + inc - v;
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const uint32_t slot = (uint32_t)(tid + j * NT), n = nl[j];
+            if (e0 + n <= (uint32_t)kPlTaskCap) {
+#pragma unroll
+                for (uint32_t l = 0; l < 4; ++l)
+                    if (l < n) tk[st][e0 + l] = (uint16_t)(slot | (l << 10));
+#pragma unroll 1
+                for (uint32_t l = 4; l < n; ++l) tk[st][e0 + l] = (uint16_t)(slot | (l << 10));
+            } else if (n) {  // over capacity: the whole workgroup walks this run
+#pragma unroll 1
+                for (uint32_t l = e0; l < (uint32_t)kPlTaskCap; ++l) tk[st][l] = kPlNoTask;
+                atomicOr(&wmask[cs][slot >> 5], 1u << (slot & 31));
+                atomicAdd(&nwhole[cs], 1u);
+            }
+            e0 += n;
         }
     };
 
-    // prologue: runs of protein 0 cut into tasks; blk of protein 1; G of protein 2
-    // DEEP: G lists loaded 2 iterations before their run-table lookups, the
-    // run-table entries 2 iterations before their tasks are cut, T words one
-    // iteration before their normalisation (register rings).
-    {
-        int32_t gt, gtB = -1;
-        uint4 r4, r4B = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t twp[KW];  // DEEP: T words of protein i-1
-        int32_t tap = 0;
-#pragma unroll
-        for (int k = 0; k < KW; ++k) twp[k] = 0u;
-        if constexpr (DEEP) {
-            const int32_t g0_ = s1(0), g1_ = s1(1), g2_ = s1(2);
-            const uint4 r0_ = s2(0, g0_);
-            r4 = s2(1, g1_);   // protein i+1 on loop entry
-            r4B = s2(2, g2_);  // protein i+2
-            gt = s1(3);        // protein i+3
-            gtB = s1(4);       // protein i+4
-            s3(0, r0_);
-        } else {
-            gt = s1(0);
-            r4 = s2(0, gt);
-            gt = s1(1);
-            s3(0, r4);
-            r4 = s2(1, gt);   // protein i+1 on loop entry
-            gt = s1(2);       // protein i+2 on loop entry
-        }
-        __syncthreads();
+    // prologue: tasks of protein 0; run-table entries of protein 1; G lists of protein 2
+    int32_t gt[EPT];
+    uint4 r4[EPT];
+    s1(0, gt);
+    s2(0, gt, r4);
+    s1(1, gt);
+    s3(0, r4);
+    s2(1, gt, r4);
+    s1(2, gt);
+    __syncthreads();
 
 #pragma unroll 1
-        for (int i = 0; i <= P; ++i) {
-            const int st = i & 1, cs = i % 3;
-            uint32_t* acc_i = acc + st * W;
-            const bool has_i = i < P && uni(goff[i + 1]) > uni(goff[i]);
-            const bool has_p = i >= 1 && uni(goff[i]) > uni(goff[i - 1]);
-            // T words of protein i-1 (normalised below, after the member loads are in flight)
-            uint32_t tw[KW];
-            const int pt = DEEP ? min(i, P - 1) : (i >= 1 ? i - 1 : 0);  // DEEP: protein i, used next iteration
-            const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
+    for (int i = 0; i <= P; ++i) {
+        const int st = i & 1, cs = i % 3;
+        uint32_t* acc_i = acc + st * W;
+        const bool has_i = i < P && glen(i) > 0u;
+        const bool has_p = i >= 1 && glen(i - 1) > 0u;
+        // T(i-1): T16 words of the thread's columns and T[p][A] (vector loads)
+        const int pt = i >= 1 ? i - 1 : 0;
+        uint32_t tw[KW];
+        const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
 #pragma unroll
-            for (int k = 0; k < KW; ++k)
-                tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (kRowThreads * 4u));
-            const int32_t ta = d.T[(int64_t)pt * d.t_cols + tca];
-            PL_TICK(0)
-            // S4 (issue): first round of member loads of protein i
-            const int nt = (has_i && !(flags & 0x400u)) ? min((int)uni(ntask[cs]), kPlTaskCap) : 0;  // 0x400: diagnostics, no member loads
-            using BT = typename std::conditional<GL == 4, uint4, int32_t>::type;
-            BT b[U];
-            uint32_t okm;
-            if constexpr (GL == 4) okm = pl_issue4<U>(r_fg, tk[st], rt[st], grp, nt - grp, gl, b);
-            else okm = pl_issue<U>(r_fg, tk[st], rt[st], grp, nt - grp, gl, b);
-            PL_TICK(1)
-            // prefetches S2, S1 (after the member loads: vmcnt retires in order)
-            const uint4 r4n = DEEP ? s2(i + 3, gt) : s2(i + 2, gt);
-            const int32_t gtn = DEEP ? s1(i + 5) : s1(i + 3);
-            PL_TICK(2)
-            // S5: normalise protein i-1
-            if (has_p && (flags & 0x100u)) {  // diagnostics: clear only
-                uint32_t* acc_p = acc + (st ^ 1) * W;
+        for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
+        const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
+        // S4a: first round of member loads of protein i (one task per 4-lane group)
+        const int nt = (has_i && !(flags & 0x400u)) ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;  // 0x400: diagnostics
+        uint4 b;
+        uint32_t okm = pl_issue(r_fg, tk[st], rt[st], grp, nt, gl, b);
+        // S3(i+1), then the prefetches S2(i+2), S1(i+3)
+        if (i + 1 < P) s3(i + 1, r4);
+        s2(i + 2, gt, r4);
+        s1(i + 3, gt);
+        // S5: normalise protein i-1 (fp64, ascending protein order per pair)
+        if (has_p) {
+            uint32_t* acc_p = acc + (st ^ 1) * W;
 #pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    const int32_t w = tid + k * kRowThreads;
-                    if (w < ncw) acc_p[w] = 0u;
-                }
-            } else if (has_p && BF) {
-                uint32_t* acc_p = acc + (st ^ 1) * W;
-                const int32_t tap_ = DEEP ? tap : ta;
-#pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    if (k * kRowThreads + (tid & ~63) < ncw) {  // wave-uniform: the wave's words exist
-                        const int32_t w = tid + k * kRowThreads;
-                        const uint32_t v = acc_p[w];
+            for (int k = 0; k < KW; ++k) {
+                const int32_t w = tid + k * NT;
+                if (w < ncw) {
+                    const uint32_t v = acc_p[w];
+                    if (v) {
                         acc_p[w] = 0u;
-                        const uint32_t t2 = DEEP ? twp[k] : tw[k];
+                        if (flags & 0x100u) continue;  // diagnostics: clear only
                         const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                        const int32_t d0 = max(tap_ + (int32_t)(t2 & 0xFFFFu) - c0, 1);
-                        const int32_t d1 = max(tap_ + (int32_t)(t2 >> 16) - c1, 1);
-                        // c = 0 adds +0.0: S is unchanged bit for bit
-                        S[2 * k] += exact_div_small((double)c0, (double)d0);
-                        S[2 * k + 1] += exact_div_small((double)c1, (double)d1);
-                        N[k] += (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 16);
-                    }
-                }
-            } else if (has_p) {
-                uint32_t* acc_p = acc + (st ^ 1) * W;
-#pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    const int32_t w = tid + k * kRowThreads;
-                    if (w < ncw) {
-                        const uint32_t v = acc_p[w];
-                        if (v) {
-                            acc_p[w] = 0u;
-                            const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                            if (c0) {
-                                S[2 * k] += (double)c0 / (double)((DEEP ? tap : ta) + (int32_t)((DEEP ? twp[k] : tw[k]) & 0xFFFFu) - c0);
-                                N[k] += 1u;
-                            }
-                            if (c1) {
-                                S[2 * k + 1] += (double)c1 / (double)((DEEP ? tap : ta) + (int32_t)((DEEP ? twp[k] : tw[k]) >> 16) - c1);
-                                N[k] += 1u << 16;
-                            }
+                        if (c0) {
+                            S[2 * k] += exact_div_small((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
+                            N[k] += 1u;
+                        }
+                        if (c1) {
+                            S[2 * k + 1] += exact_div_small((double)c1, (double)(ta + (int32_t)(tw[k] >> 16) - c1));
+                            N[k] += 1u << 16;
                         }
                     }
                 }
             }
-            PL_TICK(3)
-            // S4 (complete): atomics, further rounds, whole-workgroup runs
-            if (has_i) {
-                auto scat = [&]() {
-                    if constexpr (GL == 4 && BF) {
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const uint32_t m = okm >> (4 * u);
-                            bf_scatter<MODE>(d, a, (int32_t)b[u].x, m & 1u, acc_i, cc0, wlo, whi, ev);
-                            bf_scatter<MODE>(d, a, (int32_t)b[u].y, m & 2u, acc_i, cc0, wlo, whi, ev);
-                            bf_scatter<MODE>(d, a, (int32_t)b[u].z, m & 4u, acc_i, cc0, wlo, whi, ev);
-                            bf_scatter<MODE>(d, a, (int32_t)b[u].w, m & 8u, acc_i, cc0, wlo, whi, ev);
-                        }
-                    } else if constexpr (GL == 4) {
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const uint32_t m = okm >> (4 * u);
-                            pl_scatter<MODE>(d, a, (m & 1u) ? (int32_t)b[u].x : -1, acc_i, cc0, wlo, whi, ev, flags);
-                            pl_scatter<MODE>(d, a, (m & 2u) ? (int32_t)b[u].y : -1, acc_i, cc0, wlo, whi, ev, flags);
-                            pl_scatter<MODE>(d, a, (m & 4u) ? (int32_t)b[u].z : -1, acc_i, cc0, wlo, whi, ev, flags);
-                            pl_scatter<MODE>(d, a, (m & 8u) ? (int32_t)b[u].w : -1, acc_i, cc0, wlo, whi, ev, flags);
-                        }
-                    } else {
-#pragma unroll
-                        for (int u = 0; u < U; ++u)
-                            pl_scatter<MODE>(d, a, (okm >> u) & 1u ? b[u] : -1, acc_i, cc0, wlo, whi, ev, flags);
-                    }
-                };
-                scat();
-                for (int k0 = grp + U * NG; k0 < nt; k0 += U * NG) {
-                    if constexpr (GL == 4) okm = pl_issue4<U>(r_fg, tk[st], rt[st], k0, nt - k0, gl, b);
-                    else okm = pl_issue<U>(r_fg, tk[st], rt[st], k0, nt - k0, gl, b);
-                    scat();
-                }
-                if (uni(nwhole[cs])) {
-                    for (int wd = 0; wd < kRowThreads / 32; ++wd) {
-                        uint32_t m = uni(wmask[cs][wd]);
-                        while (m) {
-                            const int s = __builtin_ctz(m);
-                            m &= m - 1u;
-                            const uint32_t rx = uni(rt[st][wd * 32 + s].x), ry = uni(rt[st][wd * 32 + s].y);
-                            for (uint32_t mm = rx + tid; mm < ry; mm += kRowThreads)
-                                pl_scatter<MODE>(d, a, (int32_t)bld_u32(r_fg, mm * 4u, 0u), acc_i, cc0, wlo, whi, ev);
-                        }
-                    }
-                }
-            }
-            PL_TICK(4)
-            // S3: tasks of protein i+1 (last: the member ids and T words are dead here)
-            if (i + 1 < P && !(flags & 0x800u)) s3(i + 1, r4);  // 0x800: diagnostics, no tasks
-            if constexpr (DEEP) {
-                r4 = r4B;
-                r4B = r4n;
-                gt = gtB;
-                gtB = gtn;
-#pragma unroll
-                for (int k = 0; k < KW; ++k) twp[k] = tw[k];
-                tap = ta;
-            } else {
-                r4 = r4n;
-                gt = gtn;
-            }
-            // recycle the protein-(i+2) counter set (last read by S4(i-1))
-            if (tid < 32) wmask[(i + 2) % 3][tid] = 0u;
-            if (tid == 32) { ntask[(i + 2) % 3] = 0u; nwhole[(i + 2) % 3] = 0u; }
-            PL_TICK(5)
-            __syncthreads();
-            PL_TICK(6)
         }
+        // S4b: atomics of the first round, further rounds, whole-workgroup runs
+        if (has_i) {
+            pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi, ev, flags);
+            for (int k = grp + NG; k < nt; k += NG) {
+                okm = pl_issue(r_fg, tk[st], rt[st], k, nt, gl, b);
+                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi, ev, flags);
+            }
+            if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
+                for (int wd = 0; wd < kPlEntries / 32; ++wd) {
+                    uint32_t m = uni_u32(wmask[cs][wd]);
+                    while (m) {
+                        const int s = __builtin_ctz(m);
+                        m &= m - 1u;
+                        const uint32_t rx = uni_u32(rt[st][wd * 32 + s].x), ry = uni_u32(rt[st][wd * 32 + s].y);
+                        for (uint32_t mm = rx + tid; mm < ry; mm += NT)
+                            pl_add<MODE>(d, a, (int32_t)bld_u32(r_fg, mm * 4u, 0u), acc_i, cc0, wlo, whi, ev, flags);
+                    }
+                }
+            }
+        }
+        // recycle the protein-(i+2) counter set (last read by S4(i-1))
+        if (tid < kPlEntries / 32) wmask[(i + 2) % 3][tid] = 0u;
+        if (tid == 32) { ntask[(i + 2) % 3] = 0u; nwhole[(i + 2) % 3] = 0u; }
+        __syncthreads();
     }
 
-    if (prof) {
-        if (tid == 0) {
-            double* o = reinterpret_cast<double*>(s_out) + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
-            for (int k = 0; k < 7; ++k) o[k] = (double)tacc[k];
-            o[7] = (double)P;
-        }
-        return;
-    }
     // |E| of this row chunk
     ev = wave_sum_u32(ev);
     if (lane == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
@@ -492,7 +291,7 @@ __global__ __launch_bounds__(kRowThreads, PFAAI_PL_WAVES) void k_rows_pl(
     // epilogue: JAC S/N and AJI at the reference's JAC index
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
-        const int32_t w = tid + k * kRowThreads;
+        const int32_t w = tid + k * NT;
         if (w >= ncw) continue;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {

@@ -1,0 +1,84 @@
+// pfaai_util.hpp -- device helpers shared by the row kernels: raw buffer
+// loads, wave scans, run-line pruning, exact small-integer division.
+#pragma once
+#include "pfaai_kernels.hpp"
+
+namespace pfaai {
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data, no swizzle
+
+// Raw buffer loads: a 4-SGPR resource, a 32-bit per-lane byte offset and a
+// scalar byte offset instead of a 64-bit address per lane.  Out-of-range
+// offsets read 0 and fetch nothing, so loads can be issued unconditionally.
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes), kRsrcWord3);
+}
+__device__ __forceinline__ uint32_t bld_u32(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ uint4 bld_u128(rsrc_t r, uint32_t voff, uint32_t soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+}
+__device__ __forceinline__ uint32_t uni_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+
+// Inclusive wave64 prefix sum with DPP row shifts and row broadcasts.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// Run-table entry -> member range [lo, hi) and its line count after pruning
+// to the column window [wlo, whi) with the run's line splitters (k_blk).
+__device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi, uint2& r) {
+    r = make_uint2(r4.x, r4.y);
+    if (r.y - r.x <= 1u) return 0u;  // a run of one member is A alone: no partner
+    const uint32_t first = r.x & ~(uint32_t)(kGroup - 1);
+    uint32_t nl = (r.y - first + kGroup - 1) / kGroup;
+    if (nl > 1u) {
+        const uint64_t sp = (uint64_t)r4.z | ((uint64_t)r4.w << 32);
+        uint32_t l0 = 0, l1 = nl;
+#pragma unroll
+        for (uint32_t i = 1; i <= (uint32_t)kSplitters; ++i) {
+            const int32_t f = (int32_t)((sp >> (kSplitBits * (i - 1))) & kSplitNone);
+            if (i < nl) {
+                if (f <= wlo) l0 = i;            // lines < i hold ids < f <= wlo
+                if (f >= whi && l1 > i) l1 = i;  // lines >= i hold ids >= f >= whi
+            }
+        }
+        if (l1 <= l0) return 0u;
+        if (l0) r.x = first + l0 * kGroup;
+        if (l1 < nl) r.y = first + l1 * kGroup;
+        nl = l1 - l0;
+    }
+    return nl;
+}
+
+// c / d for integers 1 <= c <= 65535, c <= d < 2^17 (T < 2^16 is checked at
+// load), bit-identical to IEEE division: the same reciprocal, Newton steps
+// and final residual correction the compiler expands '/' into (v_rcp_f64,
+// 2 x fma refinement, mul, fma residual, fma correction), minus
+// v_div_scale / v_div_fmas / v_div_fixup, which are the identity for
+// operands this far from the exponent limits (no scaling, no inf / nan /
+// zero / denormal cases).  Exhaustively checked against '/' on the GPU over
+// that whole domain (pfaai_debug_div_check, tests/test_gpu_kernels.py).
+__device__ __forceinline__ double exact_div_small(double c, double dd) {
+    double y = __builtin_amdgcn_rcp(dd);
+    double e = __builtin_fma(-dd, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-dd, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    const double q = c * y;
+    const double r = __builtin_fma(-dd, q, c);
+    return __builtin_fma(r, y, q);
+}
+
+}  // namespace pfaai

@@ -4,8 +4,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-ab}
-timeout -k 10 600 python tools/gpu/ab_rows.py --genomes 10000 --rounds 4 ${AB_ARGS:---variants PFAAI_ROWS_OCC=2 PFAAI_ROWS_OCC=3 PFAAI_ROWS_OCC=4} 2>&1 | tail -6 || exit 1
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 tools/gpu/ab_rows.py --genomes 10000 --rounds 1 --variants ${PROF_VARIANT:-PFAAI_ROWS_OCC=3} > gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 600 python tools/gpu/ab_rows.py --genomes 10000 --rounds 4 ${AB_ARGS:---variants PFAAI_ROWS_KERNEL=pl PFAAI_ROWS_KERNEL=pl512} 2>&1 | tail -6 || exit 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 tools/gpu/ab_rows.py --genomes 10000 --rounds 1 --variants ${PROF_VARIANT:-PFAAI_ROWS_KERNEL=pl} > gpurun_out/prof_$TAG.log 2>&1
 rc=$?
 python3 - <<PY
 import csv

@@ -1,7 +1,7 @@
 """Interleaved A/B of k_rows variants in one process (SYN all-vs-all).
 
-    python tools/gpu/ab_rows.py --genomes 10000 --rounds 5 --variants OCC=2 OCC=1
-Each variant is an env setting read by pfaai_run (PFAAI_ROWS_OCC ...).
+    python tools/gpu/ab_rows.py --genomes 10000 --rounds 5 --variants PFAAI_ROWS_KERNEL=pl PFAAI_ROWS_KERNEL=fused
+Each variant is an env setting read by pfaai_run (PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist, PFAAI_ABLATE).
 Prints per-variant median/min of build and row-kernel device times.
 """
 import argparse
@@ -21,7 +21,7 @@ ap.add_argument("--genomes", type=int, default=10000)
 ap.add_argument("--prot", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--f-only", action="store_true")
-ap.add_argument("--variants", nargs="+", default=["PFAAI_ROWS_OCC=2", "PFAAI_ROWS_OCC=1"])
+ap.add_argument("--variants", nargs="+", default=["PFAAI_ROWS_KERNEL=pl", "PFAAI_ROWS_KERNEL=pl512"])
 a = ap.parse_args()
 g = syn.generate(a.genomes, a.prot)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${PMC_TAG:-pmc}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python3 tools/gpu/ab_rows.py --genomes ${PMC_GENOMES:-10000} --rounds 0 --variants ${PMC_VARIANT:-PFAAI_ROWS_OCC=12}"
+CMD="python3 tools/gpu/ab_rows.py --genomes ${PMC_GENOMES:-10000} --rounds 0 --variants ${PMC_VARIANT:-PFAAI_ROWS_KERNEL=pl}"
 i=0
 case "${PMC_SET:-hbm}" in
   hbm) G="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum" ;;
