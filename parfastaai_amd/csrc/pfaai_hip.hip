@@ -44,6 +44,7 @@ struct pfaai_ctx {
     // device-resident problem
     DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
     int64_t max_glen = 0;  // longest (genome, protein) G list
+    DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
     bool has_g = false;
     bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
@@ -200,8 +201,10 @@ template <int MODE>
 int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
-    HIPCHK(c, hipMemsetAsync(c->blk.p, 0, c->blk.bytes, s));
-    hipLaunchKernelGGL(k_blk, dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, err);
+    const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
+    hipLaunchKernelGGL(k_blk, dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
+                       (size_t)c->prob.n_prot * tile * sizeof(uint4), s, c->dev, tile,
+                       getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0);
     if (first_event) {
         HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
         hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
@@ -269,7 +272,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
 #define KR_CASE(K) \
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
     if (c->rows_kernel == RK_PL) {
-        switch (pick_kw<1024>(c->max_cols, 5)) {
+        const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
+        switch (pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5)) {
             case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
@@ -391,7 +395,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     if (!c) return PFAAI_OK;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&c->T16, &c->T16c, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
+    for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
@@ -536,6 +540,11 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
         if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
+        // u16 protein ids of F for k_blk's run detection (n_prot < 4096)
+        std::vector<uint16_t> fp16((size_t)p.n_f);
+        for (int64_t i = 0; i < p.n_f; ++i) fp16[i] = (uint16_t)p.F_prot[i];
+        fp16.resize((size_t)p.n_f + 16, 0);  // 16-B reads may pass the end
+        if ((rc = upload(c, c->Fp16, fp16.data(), fp16.size()))) return rc;
     }
 
     Dev& d = c->dev;
@@ -560,6 +569,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     d.G_off = c->has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
     d.G_tet = c->has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
     d.blk = c->has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
+    d.Fp16 = c->has_g ? static_cast<const uint16_t*>(c->Fp16.p) : nullptr;
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
     d.T16c = c->T16c.p ? static_cast<const uint16_t*>(c->T16c.p) : d.T16;
 
@@ -570,8 +580,16 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         for (int64_t i = 0; i < p.n_f; ++i) {
             const int32_t g = p.F_genome[i];
             if (g < 0 || g >= ni) return fail(c, PFAAI_ERR_INVALID, "F holds a genome id outside [0, n_ids)");
+            if (p.F_prot[i] < 0 || p.F_prot[i] >= p.n_prot)
+                return fail(c, PFAAI_ERR_INVALID, "F holds a protein id outside [0, n_prot)");
             fcount[g]++;
         }
+        // F sorted by (tetramer, protein, genome) -- ds_helper.hpp:126-162; the
+        // run table and the line pruning rely on it
+        for (int t = 0; t < PFAAI_NTETRAMERS; ++t)
+            for (int64_t i = p.Lp[t] + 1; i < p.Lp[t + 1]; ++i)
+                if (p.F_prot[i] < p.F_prot[i - 1] || (p.F_prot[i] == p.F_prot[i - 1] && p.F_genome[i] <= p.F_genome[i - 1]))
+                    return fail(c, PFAAI_ERR_INVALID, "F must be sorted by (tetramer, protein, genome)");
         c->row_fprefix.assign(c->n_rows + 1, 0);
         for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
         if (c->has_g) {  // work lists follow G (one record per G entry of a row genome)
@@ -641,6 +659,9 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         }
         if (!c->has_g && k != RK_WORKLIST) k = RK_WORKLIST;       // the others walk the G lists
         if (c->max_glen > kPlEntries && k != RK_WORKLIST) k = RK_FUSED;  // lists too long
+        // k_rows_pl addresses the run table with 32-bit buffer offsets
+        if ((uint64_t)c->prob.n_prot * PFAAI_NTETRAMERS * 16u >= (1ull << 32) && (k == RK_PL || k == RK_PL512))
+            k = RK_FUSED;
         c->rows_kernel = k;
     }
     if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only

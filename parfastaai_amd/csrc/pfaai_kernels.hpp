@@ -61,6 +61,7 @@ struct Dev {
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
+    const uint16_t* Fp16;       // [|F|] protein of each F entry, u16 (k_blk)
     const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)
     const uint16_t* T16c;       // same through tcol_col (ref-compat QT quirk); == T16 otherwise
     int64_t t16_cols;           // even, >= n_ids
@@ -281,63 +282,101 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 
 // ---------------------------------------------------------------------------
 // K-W1g (genome-major input): the run table.
-//   k_blk:    one workgroup per tetramer block: run heads by wavefront ballot,
-//             blk[p * 160000 + t] = {start, end, splitters} of run (t, p)
-//             in F; the splitters are the genome ids at the run's 64-B line
-//             boundaries 1..3 (21 bits each, 0x1FFFFF past the end), which
-//             let a row skip whole lines outside its column window.  The row
-//             kernels then walk each row genome's own G entries (A, p, t):
-//             the runs holding A, i.e. its E triples (ds_helper.hpp:270-357).
+//   k_blk:    blk[p * 160000 + t] = {start, end, splitters} of run (t, p) in
+//             F, one workgroup per tile of 16 tetramers: (1) run heads and
+//             tails where the protein id changes (16-B loads of u16 ids,
+//             neighbours by DPP wave shifts), (2) the splitters -- genome ids
+//             at the run's 64-B line boundaries 1..3 (21 bits each), which
+//             let a row skip whole lines outside its column window -- from
+//             one streamed id per line, (3) the tile's entries written
+//             densely (no memset pass).  p-major keeps the rows' lookups of
+//             one protein within 2.56 MB (t-major was 15 % slower in the row
+//             kernel).  0.64 ms at 10k (was 0.96 ms).  The row kernels then
+//             walk each row genome's own G entries (A, p, t): the runs
+//             holding A, i.e. its E triples (ds_helper.hpp:270-357).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int* __restrict__ err) {
-    __shared__ int32_t runs[kMaxRuns + 1];
-    __shared__ int32_t wave_cnt[kTetraThreads / 64];
-    __shared__ int32_t n_runs;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
-        const int64_t s = d.Lp[t], e = d.Lp[t + 1];
-        if (s >= e) continue;
-        if (tid == 0) n_runs = 0;
-        __syncthreads();
-        for (int64_t base = s; base < e; base += kTetraThreads) {
-            const int64_t i = base + tid;
-            bool head = false;
-            if (i < e) head = (i == s) || (d.Fp[i] != d.Fp[i - 1]);
-            const unsigned long long m = __ballot(head);
-            if (lane == 0) wave_cnt[wid] = __popcll(m);
-            __syncthreads();
-            int off = n_runs;
-            for (int w = 0; w < wid; ++w) off += wave_cnt[w];
-            if (head) {
-                const int pos = off + __popcll(m & ((1ull << lane) - 1ull));
-                if (pos < kMaxRuns) runs[pos] = (int32_t)(i - s);
-                else atomicOr(err, 1);
-            }
-            __syncthreads();
-            if (tid == 0) {
-                int add = 0;
-                for (int w = 0; w < kTetraThreads / 64; ++w) add += wave_cnt[w];
-                n_runs += add;
-            }
-            __syncthreads();
-        }
-        const int nr = min(n_runs, kMaxRuns);
-        if (tid == 0) runs[nr] = (int32_t)(e - s);
-        __syncthreads();
-        for (int j = tid; j < nr; j += kTetraThreads) {
-            const int64_t rs = s + runs[j], re = s + runs[j + 1];
-            const int64_t first = rs & ~(int64_t)(kGroup - 1);
-            uint64_t sp = 0;
+constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer for many proteins)
+constexpr int kBlkLdsBytes = 64 << 10;  // its LDS staging: n_prot x tile x 16 B
+
+// dbg (diagnostics, PFAAI_BLK_ABLATE): bit 0 skips (1), bit 1 (2), bit 2 (3).
+__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg) {
+    extern __shared__ uint4 ent[];  // [n_prot][kBlkTile] runs of the tile's tetramers
+    __shared__ int64_t lp[kBlkTileMax + 1];
+    const int tid = threadIdx.x, P = d.n_prot;
+    const int t0 = blockIdx.x * kBlkTile;
+    const int nt = min(kBlkTile, kNTetramers - t0);
+    // splitter fields start all-ones (kSplitNone); present ones are ANDed in
+    for (int k = tid; k < P * kBlkTile; k += kTetraThreads) ent[k] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0x7FFFFFFFu);
+    if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
+    __syncthreads();
+    const int64_t S = lp[0], E = lp[nt];
+    auto tet_of = [&](int64_t i) {  // tetramer of F entry i within the tile
+        int tl = 0;
+        while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
+        return tl;
+    };
+    // (1) F is sorted by (tetramer, protein, genome): a run starts where the
+    // protein changes and ends where it changes again -- each protein has one
+    // run per tetramer, so heads and tails land in slots of their own.  Each
+    // lane reads 8 consecutive u16 protein ids (one 16-B load); the ids just
+    // before and after its chunk come from the neighbouring lanes (DPP wave
+    // shifts) or, at wave edges, from one extra load.
+    const int lane = tid & 63;
+    for (int64_t c0 = (S & ~(int64_t)7) + (int64_t)tid * 8; c0 - (int64_t)lane * 8 < E && !(dbg & 1);
+         c0 += (int64_t)kTetraThreads * 8) {  // wave-uniform trip count (DPP needs the whole wave)
+        const bool in = c0 < E;
+        const uint4 v = in ? *reinterpret_cast<const uint4*>(d.Fp16 + c0) : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.w >> 16), 0x138, 0xf, 0xf, false);  // wave_shr:1
+        uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.x & 0xFFFFu), 0x130, 0xf, 0xf, false);  // wave_shl:1
+        if (lane == 0) prev = c0 > S && in ? d.Fp16[c0 - 1] : 0xFFFFu;
+        if (lane == 63) next = c0 + 8 < E ? d.Fp16[c0 + 8] : 0xFFFFu;
+        if (!in) continue;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        int tl = tet_of(max(c0, S));
 #pragma unroll
-            for (int i = 1; i <= kSplitters; ++i) {
-                const int64_t m = first + (int64_t)i * kGroup;
-                const uint64_t v = m < re ? (uint64_t)d.Fg[m] : kSplitNone;
-                sp |= v << (kSplitBits * (i - 1));
-            }
-            d.blk[(int64_t)d.Fp[rs] * kNTetramers + t] =
-                make_uint4((uint32_t)rs, (uint32_t)re, (uint32_t)sp, (uint32_t)(sp >> 32));
+        for (int j = 0; j < 8; ++j) {
+            const int64_t i = c0 + j;
+            const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            const uint32_t qp = j == 0 ? prev : (w[(j - 1) >> 1] >> (16 * ((j - 1) & 1))) & 0xFFFFu;
+            const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
+            if (i < S || i >= E) continue;
+            while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
+            if (i == lp[tl] || qp != q) ent[q * kBlkTile + tl].x = (uint32_t)i;
+            if (i + 1 == lp[tl + 1] || qn != q) ent[q * kBlkTile + tl].y = (uint32_t)(i + 1);
         }
-        __syncthreads();
+    }
+    __syncthreads();
+    constexpr int U = 8;
+    // (2) run-line splitters: the genome id at the start of lines 1..3 of
+    // every run.  Line starts are the 16-aligned F positions, so the tile's
+    // share of Fg is streamed once, one id per 64-B line, instead of being
+    // gathered run by run.
+    for (int64_t i0 = ((S + kGroup - 1) & ~(int64_t)(kGroup - 1)) + (int64_t)tid * kGroup; i0 < E && !(dbg & 2);
+         i0 += (int64_t)U * kTetraThreads * kGroup) {
+        uint32_t g[U], q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + (int64_t)u * kTetraThreads * kGroup;
+            g[u] = i < E ? (uint32_t)d.Fg[i] : 0u;
+            q[u] = i < E ? d.Fp16[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + (int64_t)u * kTetraThreads * kGroup;
+            if (i >= E) continue;
+            uint4* r = &ent[q[u] * kBlkTile + tet_of(i)];
+            const uint32_t k = (uint32_t)(i - (r->x & ~(uint32_t)(kGroup - 1))) / kGroup;  // line of the run
+            if (k < 1 || k > (uint32_t)kSplitters) continue;
+            const uint64_t field = ~(kSplitNone << (kSplitBits * (k - 1))) | ((uint64_t)g[u] << (kSplitBits * (k - 1)));
+            atomicAnd(&r->z, (uint32_t)field);
+            atomicAnd(&r->w, (uint32_t)(field >> 32));
+        }
+    }
+    __syncthreads();
+    // (3) write out: 16 consecutive entries of one protein per 256 B
+    for (int k = tid; k < P * kBlkTile && !(dbg & 4); k += kTetraThreads) {
+        const int tl = k % kBlkTile;
+        if (tl < nt) d.blk[(int64_t)(k / kBlkTile) * kNTetramers + t0 + tl] = ent[k];
     }
 }
 

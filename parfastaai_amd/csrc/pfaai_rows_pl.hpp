@@ -136,7 +136,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 
     const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)d.n_f * 4u);
     const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
-    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);
+    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked)
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);
     const rsrc_t r_t = mk_rsrc(d.T, (uint64_t)P * d.t_cols * 4u);
     // S1 / S2 return the raw loads: nothing may touch a prefetched value
@@ -219,13 +219,6 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
         const bool has_p = i >= 1 && glen(i - 1) > 0u;
-        // T(i-1): T16 words of the thread's columns and T[p][A] (vector loads)
-        const int pt = i >= 1 ? i - 1 : 0;
-        uint32_t tw[KW];
-        const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
-#pragma unroll
-        for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
-        const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
         // S4a: first round of member loads of protein i (one task per 4-lane group)
         const int nt = (has_i && !(flags & 0x400u)) ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;  // 0x400: diagnostics
         uint4 b;
@@ -234,6 +227,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         if (i + 1 < P) s3(i + 1, r4);
         s2(i + 2, gt, r4);
         s1(i + 3, gt);
+        // T(i-1): T16 words of the thread's columns and T[p][A] (vector loads)
+        const int pt = i >= 1 ? i - 1 : 0;
+        uint32_t tw[KW];
+        const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
+        const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
         // S5: normalise protein i-1 (fp64, ascending protein order per pair)
         if (has_p) {
             uint32_t* acc_p = acc + (st ^ 1) * W;
