@@ -79,9 +79,11 @@ typedef struct {
     /* Optional genome-major view (NULL if absent): the `<p>_genomes` blobs of
      * the SCP database (scp_db.hpp:219-262 reads only their lengths), as a
      * (genome, protein)-major CSR: tetramers of genome g, protein p are
-     * G_tet[G_off[g*n_prot+p] .. G_off[g*n_prot+p+1]).  With it the work
-     * lists are built without a sort (one run table + one binary search per
-     * entry); without it F is transposed on the device by a radix sort.
+     * G_tet[G_off[g*n_prot+p] .. G_off[g*n_prot+p+1]), ascending.  With it
+     * the row kernel walks genome g's tetramer list directly and looks each
+     * (protein, tetramer) run of F up in a dense run table built once per
+     * run (no sort, no per-step work lists); without it the rows are fed
+     * from work lists built from F alone (PFAAI_ROWS_KERNEL=worklist).
      * Entries whose tetramer block is absent from F are ignored. */
     const int64_t* G_off;  /* [n_ids * n_prot + 1] */
     const int32_t* G_tet;  /* [G_off[n_ids * n_prot]] */

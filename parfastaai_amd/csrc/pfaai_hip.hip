@@ -247,6 +247,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
                        flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
+
 template <int MODE, int KW>
 void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                    hipStream_t s) {
@@ -273,7 +274,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
     if (c->rows_kernel == RK_PL) {
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
-        switch (pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5)) {
+        const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+        switch (kw) {
             case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
@@ -787,12 +789,13 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
 }  // extern "C"
 
 namespace {
+template <int NS>
 __global__ void k_div_check(int32_t c_max, int32_t d_max, unsigned long long* bad) {
     const int32_t c = 1 + (int32_t)blockIdx.y;  // c <= c_max by the grid
     unsigned long long nb = 0;
     for (int64_t d = c + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d <= d_max; d += (int64_t)gridDim.x * blockDim.x) {
         const double q0 = (double)c / (double)d;
-        const double q1 = exact_div_small((double)c, (double)d);
+        const double q1 = exact_div_small<NS>((double)c, (double)d);
         nb += __double_as_longlong(q0) != __double_as_longlong(q1);
     }
     if (nb) atomicAdd(bad, nb);
@@ -810,7 +813,13 @@ int pfaai_debug_div_check(pfaai_ctx* c, int32_t c_max, int32_t d_max, int64_t* m
     if (rc) return rc;
     auto* bad = static_cast<unsigned long long*>(c->dbg.p);
     HIPCHK(c, hipMemsetAsync(bad, 0, sizeof(unsigned long long), c->stream));
-    hipLaunchKernelGGL(k_div_check, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
+    const char* ns = getenv("PFAAI_DIV_NEWTON");  // diagnostics: check a shorter refinement
+    if (ns && atoi(ns) == 0)
+        hipLaunchKernelGGL(k_div_check<0>, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
+    else if (ns && atoi(ns) == 2)
+        hipLaunchKernelGGL(k_div_check<2>, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
+    else  // the kernels' form
+        hipLaunchKernelGGL(k_div_check<1>, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
     HIPCHK(c, hipGetLastError());
     unsigned long long h = 0;
     HIPCHK(c, hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, c->stream));

@@ -12,7 +12,7 @@
 // chain is cut into stages that work on different proteins in the same
 // iteration, with ONE workgroup barrier per protein:
 //
-//   iteration i:  T(i-1)  T16 words of protein i-1 (for S5, loaded first)
+//   iteration i:  T(i-1)  T16 words of protein i-1 (for S5)
 //                 S4a(i)  issue the member-id loads of protein i's line tasks
 //                 S3(i+1) cut protein i+1's runs into 16-member line tasks
 //                         (wave scan + one LDS atomic per wave, no barrier)
@@ -20,11 +20,15 @@
 //                 S1(i+3) issue the G-list load of protein i+3
 //                 S5(i-1) normalise counter row (i-1)&1 into S, N; clear it
 //                 S4b(i)  ds_add_u32 the members into counter row i&1, then
-//                         any further task rounds and whole-workgroup runs
+//                         further task rounds (two tasks per 4-lane group in
+//                         flight) and whole-workgroup runs
 //                 barrier
 //
-// gfx9 retires vector loads in order (vmcnt), so the prefetches are issued
-// AFTER the member loads: waiting for the members never waits for them.
+// gfx9 retires vector loads in order (vmcnt), so the loads are issued in
+// the order they are consumed: T (S5), members (S4b), then the prefetches --
+// waiting for T never waits for the members, waiting for the members never
+// waits for the prefetches (T first and two tasks in flight: 12.7 -> 12.0 ms
+// at 10k).  |E| is summed from the counter rows in S5 rather than per member.
 // A line task is 16 members = 64 B; a 4-lane group takes one task and each
 // lane loads 4 members with one 16-B buffer load (a wave instruction covers
 // 16 lines), which measured 13 % faster than 16-lane groups of 4-B loads.
@@ -52,15 +56,15 @@ constexpr int kPlTaskCap = 4096;   // u16 line tasks per protein stage: run slot
 constexpr int kPlMaxLines = 63;    // runs with more lines go to the whole-workgroup walk
 constexpr uint16_t kPlNoTask = 0xFFFFu;
 
-// E triple (p, A, b): +1 into the u16 counter of column b.
+// E triple (p, A, b): +1 into the u16 counter of column b.  |E| is counted
+// from the counter rows in S5, not here (one VALU op less per member).
 template <int MODE>
 __device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint32_t* acc, int32_t cc0, int32_t wlo,
-                                       int32_t whi, uint32_t& ev, uint32_t flags) {
-    if (b < wlo || b >= whi) return;  // also drops b = -1 (no member)
+                                       int32_t whi) {
+    if ((uint32_t)(b - wlo) >= (uint32_t)(whi - wlo)) return;  // also drops b = -1 (no member)
     if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
     const uint32_t o = (uint32_t)(b - cc0);
-    if (!(flags & 0x200u)) atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));  // 0x200: diagnostics, no atomics
-    ++ev;
+    atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));
 }
 
 // Member loads of line task k of this lane's 4-lane group: 4 members (16 B)
@@ -81,11 +85,11 @@ __device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, cons
 
 template <int MODE>
 __device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, uint32_t ok, uint32_t* acc, int32_t cc0,
-                                            int32_t wlo, int32_t whi, uint32_t& ev, uint32_t flags) {
-    pl_add<MODE>(d, a, (ok & 1u) ? (int32_t)b.x : -1, acc, cc0, wlo, whi, ev, flags);
-    pl_add<MODE>(d, a, (ok & 2u) ? (int32_t)b.y : -1, acc, cc0, wlo, whi, ev, flags);
-    pl_add<MODE>(d, a, (ok & 4u) ? (int32_t)b.z : -1, acc, cc0, wlo, whi, ev, flags);
-    pl_add<MODE>(d, a, (ok & 8u) ? (int32_t)b.w : -1, acc, cc0, wlo, whi, ev, flags);
+                                            int32_t wlo, int32_t whi) {
+    pl_add<MODE>(d, a, (ok & 1u) ? (int32_t)b.x : -1, acc, cc0, wlo, whi);
+    pl_add<MODE>(d, a, (ok & 2u) ? (int32_t)b.y : -1, acc, cc0, wlo, whi);
+    pl_add<MODE>(d, a, (ok & 4u) ? (int32_t)b.z : -1, acc, cc0, wlo, whi);
+    pl_add<MODE>(d, a, (ok & 8u) ? (int32_t)b.w : -1, acc, cc0, wlo, whi);
 }
 
 template <int MODE, int KW, int NT, int WPE = 4>
@@ -219,21 +223,22 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
         const bool has_p = i >= 1 && glen(i - 1) > 0u;
-        // S4a: first round of member loads of protein i (one task per 4-lane group)
-        const int nt = (has_i && !(flags & 0x400u)) ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;  // 0x400: diagnostics
-        uint4 b;
-        uint32_t okm = pl_issue(r_fg, tk[st], rt[st], grp, nt, gl, b);
-        // S3(i+1), then the prefetches S2(i+2), S1(i+3)
-        if (i + 1 < P) s3(i + 1, r4);
-        s2(i + 2, gt, r4);
-        s1(i + 3, gt);
-        // T(i-1): T16 words of the thread's columns and T[p][A] (vector loads)
+        // T(i-1): T16 words of the thread's columns and T[p][A], issued
+        // first so that S5 waits for nothing issued after them
         const int pt = i >= 1 ? i - 1 : 0;
         uint32_t tw[KW];
         const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
 #pragma unroll
         for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
         const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
+        // S4a: first round of member loads of protein i (one task per 4-lane group)
+        const int nt = has_i ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;
+        uint4 b;
+        uint32_t okm = pl_issue(r_fg, tk[st], rt[st], grp, nt, gl, b);
+        // S3(i+1), then the prefetches S2(i+2), S1(i+3)
+        if (i + 1 < P) s3(i + 1, r4);
+        s2(i + 2, gt, r4);
+        s1(i + 3, gt);
         // S5: normalise protein i-1 (fp64, ascending protein order per pair)
         if (has_p) {
             uint32_t* acc_p = acc + (st ^ 1) * W;
@@ -244,8 +249,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     const uint32_t v = acc_p[w];
                     if (v) {
                         acc_p[w] = 0u;
-                        if (flags & 0x100u) continue;  // diagnostics: clear only
                         const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+                        ev += (uint32_t)(c0 + c1);
                         if (c0) {
                             S[2 * k] += exact_div_small((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
                             N[k] += 1u;
@@ -258,12 +263,21 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 }
             }
         }
-        // S4b: atomics of the first round, further rounds, whole-workgroup runs
+        // S4b: atomics of the first round, further rounds (two tasks per
+        // group in flight), whole-workgroup runs
         if (has_i) {
-            pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi, ev, flags);
-            for (int k = grp + NG; k < nt; k += NG) {
+            pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
+            int k = grp + NG;
+            for (; k + NG < nt; k += 2 * NG) {
+                uint4 b2;
                 okm = pl_issue(r_fg, tk[st], rt[st], k, nt, gl, b);
-                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi, ev, flags);
+                const uint32_t ok2 = pl_issue(r_fg, tk[st], rt[st], k + NG, nt, gl, b2);
+                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
+                pl_scatter4<MODE>(d, a, b2, ok2, acc_i, cc0, wlo, whi);
+            }
+            if (k < nt) {
+                okm = pl_issue(r_fg, tk[st], rt[st], k, nt, gl, b);
+                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
             }
             if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
                 for (int wd = 0; wd < kPlEntries / 32; ++wd) {
@@ -273,7 +287,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                         m &= m - 1u;
                         const uint32_t rx = uni_u32(rt[st][wd * 32 + s].x), ry = uni_u32(rt[st][wd * 32 + s].y);
                         for (uint32_t mm = rx + tid; mm < ry; mm += NT)
-                            pl_add<MODE>(d, a, (int32_t)bld_u32(r_fg, mm * 4u, 0u), acc_i, cc0, wlo, whi, ev, flags);
+                            pl_add<MODE>(d, a, (int32_t)bld_u32(r_fg, mm * 4u, 0u), acc_i, cc0, wlo, whi);
                     }
                 }
             }
@@ -284,7 +298,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         __syncthreads();
     }
 
-    // |E| of this row chunk
+    // |E| of this row chunk (the sum of its counters over all proteins)
     ev = wave_sum_u32(ev);
     if (lane == 0 && ev) atomicAdd(n_events, (unsigned long long)ev);
 

@@ -63,19 +63,25 @@ __device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi
 }
 
 // c / d for integers 1 <= c <= 65535, c <= d < 2^17 (T < 2^16 is checked at
-// load), bit-identical to IEEE division: the same reciprocal, Newton steps
+// load), bit-identical to IEEE division: the reciprocal, Newton refinement
 // and final residual correction the compiler expands '/' into (v_rcp_f64,
-// 2 x fma refinement, mul, fma residual, fma correction), minus
-// v_div_scale / v_div_fmas / v_div_fixup, which are the identity for
-// operands this far from the exponent limits (no scaling, no inf / nan /
-// zero / denormal cases).  Exhaustively checked against '/' on the GPU over
-// that whole domain (pfaai_debug_div_check, tests/test_gpu_kernels.py).
+// fma refinement, mul, fma residual, fma correction), minus v_div_scale /
+// v_div_fmas / v_div_fixup, which are the identity for operands this far
+// from the exponent limits (no scaling, no inf / nan / zero / denormal
+// cases), and with ONE Newton step instead of two: over this domain the
+// once-refined reciprocal already makes the residual correction exact.
+// Exhaustively checked against '/' on the GPU over the whole domain
+// (pfaai_debug_div_check, tests/test_gpu_kernels.py; 0 mismatches for
+// NS = 1 and 2, 2.9e9 of 4.3e9 quotients off for NS = 0).  S5 evaluates one
+// division per nonzero counter, ~5e9 at 10k, so each fma matters.
+template <int NS = 1>
 __device__ __forceinline__ double exact_div_small(double c, double dd) {
     double y = __builtin_amdgcn_rcp(dd);
-    double e = __builtin_fma(-dd, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    e = __builtin_fma(-dd, y, 1.0);
-    y = __builtin_fma(y, e, y);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const double e = __builtin_fma(-dd, y, 1.0);
+        y = __builtin_fma(y, e, y);
+    }
     const double q = c * y;
     const double r = __builtin_fma(-dd, q, c);
     return __builtin_fma(r, y, q);

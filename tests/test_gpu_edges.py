@@ -80,6 +80,13 @@ def test_qt_rectangular(engine, gm, nT, nQ):
     _check(engine, ds, compat=True)
 
 
+@GM
+def test_qt_wide_targets(engine, gm):
+    """QT rows wider than one column chunk at KW = 5 (12 000 targets)."""
+    ds = qt_syn(dict(n_tgt=12000, n_qry=16, n_prot=6, clade_size=20), genome_major=gm)
+    _check(engine, ds)
+
+
 def test_genome_without_tetramers(engine):
     """A genome with no entries at all (all its pairs have zero overlap)."""
     g = syn.generate(30, 6, clade_size=5)

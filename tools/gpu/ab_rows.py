@@ -22,6 +22,7 @@ ap.add_argument("--prot", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--f-only", action="store_true")
 ap.add_argument("--variants", nargs="+", default=["PFAAI_ROWS_KERNEL=pl", "PFAAI_ROWS_KERNEL=pl512"])
+ap.add_argument("--rows", default=None, help="row range lo:hi (default: all rows)")
 a = ap.parse_args()
 g = syn.generate(a.genomes, a.prot)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
@@ -30,6 +31,7 @@ if not a.f_only:
 eng = _capi.Engine(0)
 eng.load(**ds.problem())
 n_rows, n_pairs = eng.shape()
+r0, r1 = (int(x) for x in a.rows.split(":")) if a.rows else (0, n_rows)
 d = eng.alloc(n_pairs * 8)
 res = {v: ([], []) for v in a.variants}
 ref = None
@@ -42,7 +44,7 @@ for r in range(a.rounds + 1):
             k, val = kv.split("=")
             os.environ[k] = val
         eng.timing(reset=True)
-        eng.run(0, n_rows, 0, d)
+        eng.run(r0, r1, 0, d)
         n, b, rr = eng.timing(reset=True)
         out = eng.d2h(d, n_pairs, np.float64)
         if ref is None:
