@@ -138,7 +138,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     uint32_t ev = 0;
     __syncthreads();
 
-    const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)d.n_f * 4u);
+    // Fg carries 16 padding entries and the range covers them: a 16-B load
+    // that crosses num_records reads all zeros, not just its tail
+    const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)(d.n_f + 16) * 4u);
     const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
     const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked)
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);

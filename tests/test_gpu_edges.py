@@ -87,6 +87,35 @@ def test_qt_wide_targets(engine, gm):
     _check(engine, ds)
 
 
+def _genome_major(Lp, Fp, Fg, n_ids, P):
+    """G_off / G_tet from F: the (genome, protein) lists of ascending tetramers."""
+    t = np.repeat(np.arange(160000, dtype=np.int32), np.diff(Lp))
+    key = Fg.astype(np.int64) * P + Fp
+    order = np.argsort(key, kind="stable")  # F is tetramer-ordered: lists stay ascending
+    G_off = np.zeros(n_ids * P + 1, dtype=np.int64)
+    G_off[1:] = np.cumsum(np.bincount(key, minlength=n_ids * P))
+    return G_off, t[order]
+
+
+@pytest.mark.parametrize("k", [37, 38, 39, 40])
+def test_run_at_end_of_F(engine, k):
+    """The last run of F ends at |F| with |F| % 4 = 0..3: its final 16-B member
+    loads cross the end of the array (padding must read as data, not zeros)."""
+    g = syn.generate(61, 3, clade_size=6)
+    Lp, Fp, Fg, T = g["Lp"], g["F_prot"], g["F_genome"], g["T"].copy()
+    last = slice(Lp[159999], Lp[160000])  # replace tetramer 159999's block with one run of k genomes
+    for p_, g_ in zip(Fp[last], Fg[last]):
+        T[p_, g_] -= 1
+    Fp = np.concatenate([Fp[: Lp[159999]], np.full(k, 2, np.int32)])
+    Fg = np.concatenate([Fg[: Lp[159999]], np.arange(k, dtype=np.int32)])
+    T[2, :k] += 1
+    Lp = Lp.copy()
+    Lp[160000] = len(Fp)
+    ds = ParFAAIData.from_split(Lp, Fp, Fg, T)
+    ds.with_genome_major(*_genome_major(Lp, Fp, Fg, 61, 3))
+    _check(engine, ds)
+
+
 def test_genome_without_tetramers(engine):
     """A genome with no entries at all (all its pairs have zero overlap)."""
     g = syn.generate(30, 6, clade_size=5)
