@@ -9,14 +9,14 @@ Workload (BASELINE.json metric "10k-genome all-vs-all"): a synthetic
 20250213), all-vs-all AJI.  Every rank generates the same DB (deterministic),
 loads it into HBM once (pfaai_load), and owns a contiguous block of output
 rows balanced by pair count.  One step = the hot path over the resident
-inputs: work-list build (the reference's E construction, without E) + the
-scatter/Jaccard/AJI row kernel for the rank's rows, then (N > 1) an RCCL
-gather of the rows' fp64 AJI blocks to rank 0.  Total work is fixed as N
+inputs: the run-table build k_blk (the reference's E construction, without
+E) + the scatter/Jaccard/AJI row kernel k_rows_pl for the rank's rows, then
+(N > 1) an RCCL gather of the rows' fp64 AJI blocks to rank 0.  Total work is fixed as N
 grows: scaling "strong".  value = genome pairs of the whole matrix / max
 step time over ranks.
 
 Extra JSON objects:
-  roofline      dominant kernel k_rows: algorithmic bytes per launch
+  roofline      dominant kernel k_rows_pl: algorithmic bytes per launch
                 (8 B per E event + 8 B per AJI written) / its mean
                 duration from HIP events on the launch stream over the timed
                 region; peak 8 TB/s HBM; traffic from the committed rocprofv3
@@ -143,7 +143,7 @@ def main():
     n_f = len(g["F_genome"])
     log(f"generated SYN N={args.genomes} P={args.prot} |F|={n_f} in {time.perf_counter() - t0:.1f}s")
     ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
-    if not args.f_only:  # the DB's genome-major <p>_genomes lists: sort-free work lists
+    if not args.f_only:  # the DB's genome-major <p>_genomes lists: the row kernel walks them
         ds.with_genome_major(g["G_off"], g["G_tet"])
     eng = _capi.Engine(local)
     t0 = time.perf_counter()
