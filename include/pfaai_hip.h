@@ -156,6 +156,11 @@ int pfaai_debug_row_counts(pfaai_ctx* ctx, int64_t row, int32_t* h_counts);
  * quotient bit-identical). */
 int pfaai_debug_div_check(pfaai_ctx* ctx, int32_t c_max, int32_t d_max, int64_t* mismatches);
 
+/* Diagnostics: per-stage shader-clock sums of k_rows_pl (PFAAI_PL_CLK=1,
+ * all-vs-all, KW = 5): n == 0 arms (allocates + clears) the buffer; n > 0
+ * copies up to n u64 = [256 workgroups][16 waves][8 stages] to the host. */
+int pfaai_debug_clocks(pfaai_ctx* ctx, uint64_t* out, int64_t n);
+
 /* Device memory helpers (so callers without a GPU framework can run the
  * device-resident path): allocate/free on the context's device, copy. */
 int pfaai_device_alloc(pfaai_ctx* ctx, void** ptr, int64_t bytes);

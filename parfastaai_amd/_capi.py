@@ -30,7 +30,7 @@ FLAG_EMIT_JAC = 2
 EXPORTS = [
     "pfaai_version", "pfaai_create", "pfaai_destroy", "pfaai_last_error", "pfaai_load",
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
-    "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
+    "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing",
 ]
 
@@ -78,6 +78,7 @@ def load_library():
         "pfaai_last_stats": (ctypes.c_int, [vp, P64, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
         "pfaai_debug_row_counts": (ctypes.c_int, [vp, i64, vp]),
         "pfaai_debug_div_check": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32, vp]),
+        "pfaai_debug_clocks": (ctypes.c_int, [vp, vp, ctypes.c_int64]),
         "pfaai_device_alloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), i64]),
         "pfaai_device_free": (ctypes.c_int, [vp, vp]),
         "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
@@ -187,6 +188,16 @@ class Engine:
         n = ctypes.c_int64()
         self._check(self.lib.pfaai_debug_div_check(self.ctx, c_max, d_max, ctypes.byref(n)), "pfaai_debug_div_check")
         return n.value
+
+    def debug_clocks(self, arm=False):
+        """k_rows_pl stage clocks (PFAAI_PL_CLK=1): arm=True clears the buffer;
+        otherwise returns u64 [256 workgroups, 16 waves, 8 stages]."""
+        if arm:
+            self._check(self.lib.pfaai_debug_clocks(self.ctx, None, 0), "pfaai_debug_clocks")
+            return None
+        out = np.zeros((256, 16, 8), dtype=np.uint64)
+        self._check(self.lib.pfaai_debug_clocks(self.ctx, _ptr(out), out.size), "pfaai_debug_clocks")
+        return out
 
     def debug_row_counts(self, row, n_prot, n_ids):
         out = np.zeros((n_prot, n_ids), dtype=np.int32)

@@ -275,6 +275,16 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     if (c->rows_kernel == RK_PL) {
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+        if (MODE == 0 && kw == 5 && getenv("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+            const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
+            const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
+            auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
+                               chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
+                               static_cast<unsigned long long*>(c->dbg.p));
+            return;
+        }
         switch (kw) {
             case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
@@ -825,6 +835,22 @@ int pfaai_debug_div_check(pfaai_ctx* c, int32_t c_max, int32_t d_max, int64_t* m
     HIPCHK(c, hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *mismatches = (int64_t)h;
+    return PFAAI_OK;
+}
+
+int pfaai_debug_clocks(pfaai_ctx* c, uint64_t* out, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !out)) return PFAAI_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t cap = (int64_t)kClkBlocks * 16 * 8;
+    if (n == 0) {  // arm: allocate and clear the clock buffer
+        int rc = ensure(c, c->dbg, cap * sizeof(uint64_t));
+        if (rc) return rc;
+        HIPCHK(c, hipMemset(c->dbg.p, 0, cap * sizeof(uint64_t)));
+        return PFAAI_OK;
+    }
+    if (c->dbg.bytes < (size_t)cap * sizeof(uint64_t)) return fail(c, PFAAI_ERR_INVALID, "clocks not armed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->dbg.p, std::min(n, cap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PFAAI_OK;
 }
 

@@ -92,12 +92,19 @@ __device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, ui
     pl_add<MODE>(d, a, (ok & 8u) ? (int32_t)b.w : -1, acc, cc0, wlo, whi);
 }
 
-template <int MODE, int KW, int NT, int WPE = 4>
+// CLK (diagnostics, PFAAI_PL_CLK): every wave of the first kClkBlocks
+// workgroups sums the shader-clock time of each stage of the protein loop
+// into clk[(block * (NT / 64) + wave) * 8 + stage] (pfaai_debug_clocks,
+// tools/gpu/stage_clocks.py).
+constexpr int kClkBlocks = 256;
+
+template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
                                                    double* __restrict__ aji, double* __restrict__ s_out,
                                                    int32_t* __restrict__ n_out,
-                                                   unsigned long long* __restrict__ n_events) {
+                                                   unsigned long long* __restrict__ n_events,
+                                                   unsigned long long* __restrict__ clk = nullptr) {
     constexpr int W = KW * NT;            // counter words per row chunk
     constexpr int EPT = kPlEntries / NT;  // G entries per thread
     constexpr int NG = NT / 4;            // 4-lane groups
@@ -219,6 +226,15 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     s1(2, gt);
     __syncthreads();
 
+    unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = CLK ? clock64() : 0;
+    auto stamp = [&](int j) {
+        if constexpr (CLK) {
+            const unsigned long long t = clock64();
+            ck[j] += t - tprev;
+            tprev = t;
+        }
+    };
 #pragma unroll 1
     for (int i = 0; i <= P; ++i) {
         const int st = i & 1, cs = i % 3;
@@ -237,10 +253,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         const int nt = has_i ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;
         uint4 b;
         uint32_t okm = pl_issue(r_fg, tk[st], rt[st], grp, nt, gl, b);
+        stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
         if (i + 1 < P) s3(i + 1, r4);
+        stamp(1);
         s2(i + 2, gt, r4);
         s1(i + 3, gt);
+        stamp(2);
         // S5: normalise protein i-1 (fp64, ascending protein order per pair)
         if (has_p) {
             uint32_t* acc_p = acc + (st ^ 1) * W;
@@ -265,10 +284,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 }
             }
         }
+        stamp(3);
         // S4b: atomics of the first round, further rounds (two tasks per
         // group in flight), whole-workgroup runs
         if (has_i) {
             pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
+            stamp(4);
             int k = grp + NG;
             for (; k + NG < nt; k += 2 * NG) {
                 uint4 b2;
@@ -294,10 +315,16 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 }
             }
         }
+        stamp(5);
         // recycle the protein-(i+2) counter set (last read by S4(i-1))
         if (tid < kPlEntries / 32) wmask[(i + 2) % 3][tid] = 0u;
         if (tid == 32) { ntask[(i + 2) % 3] = 0u; nwhole[(i + 2) % 3] = 0u; }
         __syncthreads();
+        stamp(6);
+    }
+    if constexpr (CLK) {
+        if (lane == 0 && blockIdx.x < kClkBlocks && blockIdx.y == 0)
+            for (int j = 0; j < 7; ++j) clk[((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 8 + j] = ck[j];
     }
 
     // |E| of this row chunk (the sum of its counters over all proteins)
