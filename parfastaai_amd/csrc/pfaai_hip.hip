@@ -236,14 +236,14 @@ int pick_kw(int32_t max_cols, int kw_max) {
     return kw_max;
 }
 
-template <int MODE, int KW, int NT, int WPE = 4>
+template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
-    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t);
+    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev, rb, chunk,
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev, rb, chunk,
                        flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
@@ -283,6 +283,18 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
                                chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
                                static_cast<unsigned long long*>(c->dbg.p));
+            return;
+        }
+        // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
+        const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
+        if (nl) {
+            switch (kw) {
+                case 1: launch_pl<MODE, 1, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 2: launch_pl<MODE, 2, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 3: launch_pl<MODE, 3, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 4: launch_pl<MODE, 4, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                default: launch_pl<MODE, 5, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+            }
             return;
         }
         switch (kw) {

@@ -70,9 +70,10 @@ __device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint3
 // Member loads of line task k of this lane's 4-lane group: 4 members (16 B)
 // of the task's 64-B line, issued unconditionally (an out-of-range offset
 // where the lane has none).  Bit j of the result: member j of b is valid.
+template <int TC = kPlTaskCap>
 __device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k, int nt, int gl,
                                              uint4& b) {
-    const uint32_t t = tk[min(k, kPlTaskCap - 1)];
+    const uint32_t t = tk[min(k, TC - 1)];
     const uint2 rr = rt[t & 1023u];
     const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + (t >> 10) * kGroup + 4u * (uint32_t)gl;
     const bool task = k < nt && t != kPlNoTask;
@@ -98,7 +99,9 @@ __device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, ui
 // tools/gpu/stage_clocks.py).
 constexpr int kClkBlocks = 256;
 
-template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false>
+// NL: the per-column counts N live in LDS (u8 pairs, P <= 255) instead of
+// registers -- 5 VGPRs less at KW = 5, paid for with half the task capacity.
+template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
                                                    double* __restrict__ aji, double* __restrict__ s_out,
@@ -108,9 +111,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr int W = KW * NT;            // counter words per row chunk
     constexpr int EPT = kPlEntries / NT;  // G entries per thread
     constexpr int NG = NT / 4;            // 4-lane groups
-    extern __shared__ uint32_t pl_smem[];                // acc[2][W], goff[P + 1]
+    constexpr int TC = NL ? kPlTaskCap / 2 : kPlTaskCap;  // line tasks per stage
+    extern __shared__ uint32_t pl_smem[];                // acc[2][W], goff[P + 1], (NL) n16[W]
     __shared__ uint2 rt[2][kPlEntries];                  // runs of a protein stage: member range [lo, hi)
-    __shared__ uint16_t tk[2][kPlTaskCap];               // line tasks
+    __shared__ uint16_t tk[2][TC];                       // line tasks
     __shared__ uint32_t wmask[3][kPlEntries / 32];       // whole-workgroup runs, by protein % 3
     __shared__ uint32_t ntask[3], nwhole[3];             // by protein % 3
 
@@ -129,19 +133,24 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
+    uint16_t* n16 = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1);  // NL: N of columns (2w, 2w+1) as u8 pair
 
     const int64_t g0 = d.G_off[(int64_t)a * P];
     for (int p = tid; p <= P; p += NT) goff[p] = (uint32_t)(d.G_off[(int64_t)a * P + p] - g0);
     for (int w = tid; w < 2 * W; w += NT) acc[w] = 0u;
+    if (NL)
+        for (int w = tid; w < W; w += NT) n16[w] = 0u;
     if (tid < 3) { ntask[tid] = 0u; nwhole[tid] = 0u; }
     for (int w = tid; w < 3 * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
     const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
     const uint16_t* T16 = compat ? d.T16c : d.T16;
     const int64_t t16w = d.t16_cols >> 1;            // u32 words per protein row of T16
     double S[2 * KW];
-    uint32_t N[KW];  // packed u16 pair counts
+    uint32_t N[NL ? 1 : KW];  // packed u16 pair counts (registers unless NL)
 #pragma unroll
-    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; N[k] = 0u; }
+    for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; }
+#pragma unroll
+    for (int k = 0; k < (NL ? 1 : KW); ++k) N[k] = 0u;
     uint32_t ev = 0;
     __syncthreads();
 
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const uint32_t slot = (uint32_t)(tid + j * NT), n = nl[j];
-            if (e0 + n <= (uint32_t)kPlTaskCap) {
+            if (e0 + n <= (uint32_t)TC) {
 #pragma unroll
                 for (uint32_t l = 0; l < 4; ++l)
                     if (l < n) tk[st][e0 + l] = (uint16_t)(slot | (l << 10));
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 for (uint32_t l = 4; l < n; ++l) tk[st][e0 + l] = (uint16_t)(slot | (l << 10));
             } else if (n) {  // over capacity: the whole workgroup walks this run
 #pragma unroll 1
-                for (uint32_t l = e0; l < (uint32_t)kPlTaskCap; ++l) tk[st][l] = kPlNoTask;
+                for (uint32_t l = e0; l < (uint32_t)TC; ++l) tk[st][l] = kPlNoTask;
                 atomicOr(&wmask[cs][slot >> 5], 1u << (slot & 31));
                 atomicAdd(&nwhole[cs], 1u);
             }
@@ -250,9 +259,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
         const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
         // S4a: first round of member loads of protein i (one task per 4-lane group)
-        const int nt = has_i ? min((int)uni_u32(ntask[cs]), kPlTaskCap) : 0;
+        const int nt = has_i ? min((int)uni_u32(ntask[cs]), TC) : 0;
         uint4 b;
-        uint32_t okm = pl_issue(r_fg, tk[st], rt[st], grp, nt, gl, b);
+        uint32_t okm = pl_issue<TC>(r_fg, tk[st], rt[st], grp, nt, gl, b);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
         if (i + 1 < P) s3(i + 1, r4);
@@ -272,13 +281,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                         acc_p[w] = 0u;
                         const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                         ev += (uint32_t)(c0 + c1);
+                        if constexpr (NL) n16[w] = (uint16_t)(n16[w] + (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 8));
                         if (c0) {
                             S[2 * k] += exact_div_small((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
-                            N[k] += 1u;
+                            if constexpr (!NL) N[k] += 1u;
                         }
                         if (c1) {
                             S[2 * k + 1] += exact_div_small((double)c1, (double)(ta + (int32_t)(tw[k] >> 16) - c1));
-                            N[k] += 1u << 16;
+                            if constexpr (!NL) N[k] += 1u << 16;
                         }
                     }
                 }
@@ -293,13 +303,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             int k = grp + NG;
             for (; k + NG < nt; k += 2 * NG) {
                 uint4 b2;
-                okm = pl_issue(r_fg, tk[st], rt[st], k, nt, gl, b);
-                const uint32_t ok2 = pl_issue(r_fg, tk[st], rt[st], k + NG, nt, gl, b2);
+                okm = pl_issue<TC>(r_fg, tk[st], rt[st], k, nt, gl, b);
+                const uint32_t ok2 = pl_issue<TC>(r_fg, tk[st], rt[st], k + NG, nt, gl, b2);
                 pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
                 pl_scatter4<MODE>(d, a, b2, ok2, acc_i, cc0, wlo, whi);
             }
             if (k < nt) {
-                okm = pl_issue(r_fg, tk[st], rt[st], k, nt, gl, b);
+                okm = pl_issue<TC>(r_fg, tk[st], rt[st], k, nt, gl, b);
                 pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
             }
             if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
@@ -342,7 +352,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             if (b < wlo || b >= whi || !col_valid<MODE>(d, a, b)) continue;
             const int64_t idx = pair_index<MODE>(d, a, b, compat);
             double s = S[2 * k + h];
-            int32_t n = (int32_t)((N[k] >> (16 * h)) & 0xFFFFu);
+            int32_t n = NL ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu) : (int32_t)((N[NL ? 0 : k] >> (16 * h)) & 0xFFFFu);
             if (n == 0 && compat) {
                 // extents stay 0/0 -> J of E[0]'s protein, N = 1
                 const unsigned long long key = *first_key;

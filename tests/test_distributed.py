@@ -64,9 +64,14 @@ def test_split_rows_balanced():
         blocks = split_rows(n, w)
         assert blocks[0][0] == 0 and blocks[-1][1] == n
         assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
-        pairs = [sum(n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
+        k = 0.75 * n  # shard.FIXED_COST_FRACTION
+        cost = [sum(k + n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
         if n >= 100 * w:
-            assert max(pairs) - min(pairs) <= n  # within one row
+            assert max(cost) - min(cost) <= 2 * (k + n)  # within a row or two
+    # pure pair balance with fixed_cols = 0
+    blocks = split_rows(10000, 8, fixed_cols=0)
+    pairs = [sum(10000 - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
+    assert max(pairs) - min(pairs) <= 10000
     assert split_rows(10, 3, all_vs_all=False) == [(0, 3), (3, 6), (6, 10)]
 
 

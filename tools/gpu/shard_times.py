@@ -1,0 +1,37 @@
+"""Per-shard device times of the row kernel for split_rows(n, world) at 10k:
+checks the row cost model of parfastaai_amd/shard.py on one GPU (each shard
+run alone, as one rank of a world-size run would)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+from parfastaai_amd import _capi, syn  # noqa: E402
+from parfastaai_amd.datastruct import ParFAAIData  # noqa: E402
+from parfastaai_amd.shard import split_rows  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+world = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+g = syn.generate(n, 100)
+ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
+eng = _capi.Engine(0)
+eng.load(**ds.problem())
+rows, pairs = eng.shape()
+d = eng.alloc(pairs * 8)
+eng.run(0, rows, 0, d)
+for label, kw in (("cost model", {}), ("pair balance", {"fixed_cols": 0})):
+    blocks = split_rows(rows, world, **kw)
+    ms = []
+    for rb, re_ in blocks:
+        t = []
+        for _ in range(3):
+            eng.timing(reset=True)
+            eng.run(rb, re_, 0, d)
+            _, b, r = eng.timing(reset=True)
+            t.append(r)
+        ms.append(float(np.median(t)))
+    print(f"{label:12s} rows/shard {[b1 - b0 for b0, b1 in blocks]}")
+    print(f"{label:12s} k_rows ms  {[round(x, 3) for x in ms]}  max {max(ms):.3f}  mean {np.mean(ms):.3f}")
+eng.free(d)
