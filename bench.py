@@ -8,12 +8,14 @@ Workload (BASELINE.json metric "10k-genome all-vs-all"): a synthetic
 10,000-genome x 100-SCP database (SURVEY.md §8d SYN generator, seed
 20250213), all-vs-all AJI.  Every rank generates the same DB (deterministic),
 loads it into HBM once (pfaai_load), and owns a contiguous block of output
-rows balanced by pair count.  One step = the hot path over the resident
-inputs: the run-table build k_blk (the reference's E construction, without
-E) + the scatter/Jaccard/AJI row kernel k_rows_pl for the rank's rows, then
-(N > 1) an RCCL gather of the rows' fp64 AJI blocks to rank 0.  Total work is fixed as N
-grows: scaling "strong".  value = genome pairs of the whole matrix / max
-step time over ranks.
+rows balanced by a measured row-cost model (parfastaai_amd/shard.py).  One
+step = the hot path over the resident inputs: the run-table build k_blk (the
+reference's E construction, without E) + the scatter/Jaccard/AJI row kernel
+k_rows_pl over the rank's rows; for N > 1 the rows run in --chunks pipeline
+chunks (the run table built once per step) and each chunk's fp64 AJI is
+gathered to rank 0 over RCCL asynchronously while the next chunk computes.
+Total work is fixed as N grows: scaling "strong".  value = genome pairs of
+the whole matrix / max step time over ranks.
 
 Extra JSON objects:
   roofline      dominant kernel k_rows_pl: algorithmic bytes per launch
@@ -52,11 +54,13 @@ def log(msg):
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
-def traffic_from_profiles():
+def traffic_from_profiles(genomes, prot, world):
     """HBM bytes per k_rows launch from profiles/pmc_k_rows.json (written by
-    tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes)."""
+    tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes).
+    The passes profile one launch over all rows of the 10k x 100 workload:
+    any other shape reports null."""
     p = os.path.join(ROOT, "profiles", "pmc_k_rows.json")
-    if not os.path.exists(p):
+    if not os.path.exists(p) or (genomes, prot, world) != (10000, 100, 1):
         return None
     try:
         with open(p) as f:
@@ -120,6 +124,8 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=320)
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N > 1: pipeline chunks per rank (gather of chunk j overlaps chunk j+1)")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     args = ap.parse_args()
@@ -136,7 +142,7 @@ def main():
 
     from parfastaai_amd import _capi, syn
     from parfastaai_amd.datastruct import ParFAAIData
-    from parfastaai_amd.shard import split_rows
+    from parfastaai_amd.shard import PipelinedGather, split_range, split_rows
 
     t0 = time.perf_counter()
     g = syn.generate(args.genomes, args.prot)
@@ -155,27 +161,40 @@ def main():
     spans = [eng.row_span(rb, re) for rb, re in blocks]
     rb, re = blocks[rank]
     first, count = spans[rank]
-    maxcount = max(c for _, c in spans)
-    out = torch.zeros(max(maxcount, 1), dtype=torch.float64, device=dev)
-    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # N > 1: the rank's rows in pipeline chunks; chunk j's AJI is gathered to
+    # rank 0 (RCCL, async) while chunk j+1 computes; the run table is built
+    # by chunk 0 only (PFAAI_FLAG_KEEP_RUNS)
+    nch = 1 if world == 1 else max(1, args.chunks)
+    sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
+    counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
+    pg = PipelinedGather(counts, dst=0, device=dev)
     stream = torch.cuda.current_stream(dev)
-    base = out.data_ptr() - first * 8  # pfaai_run indexes by the global JAC index
+    # pfaai_run indexes by the global JAC index: chunk j writes its own buffer
+    bases = [pg.bufs[j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
 
     def step():
-        eng.run(rb, re, 0, base, stream=stream.cuda_stream)
-        if world > 1:
-            dist.gather(out, gather, dst=0)
+        for j, (c0, c1) in enumerate(sub[rank]):
+            if c1 > c0:
+                eng.run(c0, c1, _capi.FLAG_KEEP_RUNS if j else 0, bases[j], stream=stream.cuda_stream)
+            pg.issue(j)
+        pg.wait()
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[local])
 
+    # |E| of this rank's rows: one untimed pass, chunk by chunk
+    n_events = 0
+    for j, (c0, c1) in enumerate(sub[rank]):
+        if c1 > c0:
+            eng.run(c0, c1, 0, bases[j], stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            n_events += eng.stats()["n_events"]
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     barrier()
     eng.timing(reset=True)
-    n_events = eng.stats()["n_events"]  # per run, rank-local
 
     barrier()
     torch.cuda.synchronize(dev)
@@ -187,6 +206,8 @@ def main():
     barrier()
     elapsed = t1 - t0
     n_runs, ms_build, ms_rows = eng.timing(reset=True)
+    # per step: the rank's k_blk (once) and its k_rows_pl launches (one per chunk)
+    n_runs = args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -205,20 +226,17 @@ def main():
 
     if rank == 0:
         # spot-check the gathered / local result for sanity (cheap properties)
-        if world > 1:
-            vals = torch.cat([gather[r][: spans[r][1]] for r in range(world)])
-        else:
-            vals = out[:count]
+        vals = pg.result()
         vmin, vmax = float(vals.min().item()), float(vals.max().item())
         assert vals.numel() == n_pairs and 0.0 <= vmin and vmax <= 1.0, (vals.numel(), vmin, vmax)
 
-        k_rows_ms = ms_rows / max(n_runs, 1)  # rank 0's own k_rows launch duration
+        k_rows_ms = ms_rows / max(n_runs, 1)  # rank 0's own k_rows launch(es) per step
         rank_pairs = count
         alg_bytes = 8 * n_events + 8 * rank_pairs
         achieved = alg_bytes / (k_rows_ms * 1e-3) / 1e9
         step_bytes = 8 * total_events + 4 * n_f + 8 * n_pairs  # SURVEY §8d B_alg
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(),
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.genomes, args.prot, world),
                     "kernel": ROWS_KERNEL,
                     "kernel_ms": round(k_rows_ms, 4), "alg_bytes_per_launch": alg_bytes,
                     "build_kernels_ms": round(ms_build / max(n_runs, 1), 4)}

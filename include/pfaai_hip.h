@@ -52,6 +52,9 @@ enum { PFAAI_MODE_ALL = 0, PFAAI_MODE_QSUB = 1, PFAAI_MODE_QT = 2 };
 /* Run flags */
 #define PFAAI_FLAG_REF_COMPAT 1u /* reproduce reference quirks */
 #define PFAAI_FLAG_EMIT_JAC 2u   /* also write the JAC S (f64) and N (i32) */
+#define PFAAI_FLAG_KEEP_RUNS 4u  /* reuse the run table an earlier pfaai_run on this
+                                    load built (same stream or ordered after it):
+                                    row tiles / pipelined shards pay k_blk once */
 
 typedef struct pfaai_ctx pfaai_ctx;
 
@@ -68,7 +71,7 @@ typedef struct {
     int32_t t_cols;        /* columns of T (T is P x t_cols, row-major) */
     int32_t n_qry;         /* QSUB: |query list|; QT: genomes of the query DB */
     int32_t n_tgt;         /* QSUB: n_ids - n_qry; QT: genomes of the target DB; ALL: unused */
-    int64_t n_f;           /* |F| (must be < 2^31) */
+    int64_t n_f;           /* |F| (<= 2^32 - 64) */
     const int64_t* Lp;     /* [PFAAI_NTETRAMERS + 1] exclusive prefix of Lc, Lp[160000] = n_f */
     const int32_t* F_prot; /* [n_f] F[i].first  (protein index) */
     const int32_t* F_genome; /* [n_f] F[i].second (genome id) */
@@ -129,6 +132,26 @@ int pfaai_run(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags
  * (algorithm_impl.hpp:325-329). */
 int pfaai_compute(pfaai_ctx* ctx, uint32_t flags, double* h_aji, double* h_S,
                   int32_t* h_N);
+
+/*
+ * Output-tile streaming (the output too large
+ * to hold whole).  Rows [row_begin, row_end) are cut into row tiles of at
+ * most tile_pairs JAC entries (at least one row each); every tile is
+ * computed on the device, copied to pinned host memory while the next tile
+ * computes, and handed to sink() in row order on the calling thread:
+ *   sink(user, tile_row_begin, tile_row_end, first, count, aji, S, N)
+ * with aji[i] (and, under PFAAI_FLAG_EMIT_JAC, S[i], N[i]) the pair at JAC
+ * index first + i (ds_impl.hpp:83-86, 411-413).  The host arrays are valid
+ * only during the sink call.  A non-zero sink return stops the stream and
+ * is returned.  ALL and QT modes (contiguous row spans).  Synchronous; the
+ * device holds two tiles, never the whole output.
+ */
+typedef int (*pfaai_sink_fn)(void* user, int64_t row_begin, int64_t row_end, int64_t first,
+                             int64_t count, const double* aji, const double* S, const int32_t* N);
+int pfaai_stream(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, int64_t tile_pairs,
+                 uint32_t flags, pfaai_sink_fn sink, void* user);
+/* |E| summed over the tiles of the last pfaai_stream. */
+int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 
 /* |E| of the last run, counted by the scatter kernel (equals the reference's
  * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and

@@ -16,6 +16,7 @@
 // DSIT (pfaai_mode_of<DSIT>) or passed explicitly.
 #pragma once
 #include <cstdint>
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -80,6 +81,31 @@ class ParFAAIHipImpl {
         computeJAC();
         computeAJI();
         return 0;
+    }
+    // Output-tile streaming (pfaai_stream): the AJI vector
+    // in JAC-index order written to `path` in the reference's cereal
+    // vector<double> format (u64 count + doubles, as PREFIX_aji.bin), tile by
+    // tile -- neither the host nor the device holds the whole output.  ALL and
+    // QT modes.  Returns 0, or the engine / I/O error code.
+    int streamAJI(const std::string& path, int64_t tile_pairs) {
+        int64_t rows = 0, pairs = 0;
+        int rc = pfaai_shape(m_ctx, &rows, &pairs);
+        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        FILE* f = std::fopen(path.c_str(), "wb");
+        if (!f) return PFAAI_ERR_INVALID;
+        const uint64_t n = (uint64_t)pairs;
+        bool ok = std::fwrite(&n, 8, 1, f) == 1;
+        auto sink = [](void* user, int64_t, int64_t, int64_t, int64_t count, const double* aji, const double*,
+                       const int32_t*) -> int {
+            return std::fwrite(aji, sizeof(double), (size_t)count, static_cast<FILE*>(user)) == (size_t)count
+                       ? 0 : PFAAI_ERR_INVALID;
+        };
+        rc = ok ? pfaai_stream(m_ctx, 0, rows, tile_pairs, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, sink, f)
+                : PFAAI_ERR_INVALID;
+        ok = std::fclose(f) == 0 && ok;
+        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        pfaai_stream_events(m_ctx, &m_events);
+        return ok ? 0 : PFAAI_ERR_INVALID;
     }
     const std::vector<JACType>& getJAC() const { return m_JAC; }
     const std::vector<ValueType>& getAJI() const { return m_AJI; }

@@ -25,14 +25,21 @@ ERR_NAMES = {1: "SQLITE_DB", 2: "SQLITE_MEM_ALLOC", 3: "CONSTRUCT", 4: "HIP", 5:
 MODE_ALL, MODE_QSUB, MODE_QT = 0, 1, 2
 FLAG_REF_COMPAT = 1
 FLAG_EMIT_JAC = 2
+FLAG_KEEP_RUNS = 4
 
 # every symbol include/pfaai_hip.h declares
 EXPORTS = [
     "pfaai_version", "pfaai_create", "pfaai_destroy", "pfaai_last_error", "pfaai_load",
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
-    "pfaai_synchronize", "pfaai_timing",
+    "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
 ]
+
+# int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
+#          const double* S, const int32_t* N)   (pfaai_sink_fn)
+SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                           ctypes.c_int64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                           ctypes.POINTER(ctypes.c_int32))
 
 
 class PfaaiError(RuntimeError):
@@ -83,6 +90,8 @@ def load_library():
         "pfaai_device_free": (ctypes.c_int, [vp, vp]),
         "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
         "pfaai_synchronize": (ctypes.c_int, [vp]),
+        "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
+        "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     }
@@ -169,6 +178,33 @@ class Engine:
         """Device-resident run; d_* are device pointers (ints), stream a hipStream_t (int)."""
         self._check(self.lib.pfaai_run(self.ctx, row_begin, row_end, flags, d_aji, d_S, d_N, stream),
                     "pfaai_run")
+
+    def stream(self, row_begin, row_end, tile_pairs, flags, sink):
+        """Output-tile streaming (pfaai_stream): sink(row_begin, row_end, first,
+        aji, S, N) gets numpy views of each tile in row order (valid during the
+        call only; S, N are None without FLAG_EMIT_JAC); a truthy return stops
+        the stream.  Returns |E| over all tiles."""
+        jac = bool(flags & FLAG_EMIT_JAC)
+        err = []
+
+        def _cb(_user, rb, re, first, count, aji, S, N):
+            try:
+                a = np.ctypeslib.as_array(aji, shape=(count,)) if count else np.zeros(0)
+                s_ = np.ctypeslib.as_array(S, shape=(count,)) if (jac and count) else None
+                n_ = np.ctypeslib.as_array(N, shape=(count,)) if (jac and count) else None
+                return 7 if sink(rb, re, first, a, s_, n_) else 0
+            except Exception as e:  # surfaced after the call
+                err.append(e)
+                return 7
+
+        cb = SINK_FN(_cb)
+        rc = self.lib.pfaai_stream(self.ctx, row_begin, row_end, int(tile_pairs), flags, cb, None)
+        if err:
+            raise err[0]
+        self._check(rc, "pfaai_stream")
+        ne = ctypes.c_int64()
+        self._check(self.lib.pfaai_stream_events(self.ctx, ctypes.byref(ne)), "pfaai_stream_events")
+        return ne.value
 
     def stats(self):
         ne, mb, mr = ctypes.c_int64(), ctypes.c_float(), ctypes.c_float()

@@ -47,6 +47,8 @@ struct pfaai_ctx {
     DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
     bool has_g = false;
+    bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
+    bool runs_key = false;
     bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
     Dev dev{};
 
@@ -56,6 +58,13 @@ struct pfaai_ctx {
     DevBuf out_aji, out_S, out_N, dbg;
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
+    // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t st_done[2] = {nullptr, nullptr}, st_copied[2] = {nullptr, nullptr};
+    void* st_host = nullptr;
+    size_t st_host_bytes = 0;
+    DevBuf st_dev;
+    int64_t st_events = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool timed = false;
     int rows_kernel = 0;  // RowsKernel of the current run
@@ -72,6 +81,8 @@ namespace {
 // G lists longer than k_rows_pl does; WORKLIST (k_rows<false> over sorted
 // work lists) serves F-only input.  PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist
 // overrides the choice (A/B runs, tools/gpu/ab_rows.py; tests).
+constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
+
 enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
 
 // scalars buffer layout (u64 each)
@@ -243,8 +254,14 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
     const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev, rb, chunk,
-                       flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
+    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    if (bigf)
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, true>), dim3(re - rb, nchunks), dim3(NT), lds, s,
+                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else
+        hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev,
+                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
 
@@ -377,7 +394,17 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         const int rcw = ensure_worklists(c);
         if (rcw) return rcw;
     }
-    int rc = wl ? build_records<MODE>(c, rb, re, s, compat) : build_runs_g<MODE>(c, s, compat);
+    // PFAAI_FLAG_KEEP_RUNS: the run table depends only on the loaded F, so a
+    // run over further rows of the same problem may reuse it (stream-ordered
+    // after the run that built it)
+    const bool keep = !wl && (flags & PFAAI_FLAG_KEEP_RUNS) && c->runs_valid && (c->runs_key || !compat);
+    int rc = PFAAI_OK;
+    if (wl) rc = build_records<MODE>(c, rb, re, s, compat);
+    else if (!keep) {
+        rc = build_runs_g<MODE>(c, s, compat);
+        c->runs_valid = rc == PFAAI_OK;
+        c->runs_key = compat;
+    }
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
@@ -425,6 +452,13 @@ int pfaai_destroy(pfaai_ctx* c) {
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
+    release(c->st_dev);
+    if (c->st_host) (void)hipHostFree(c->st_host);
+    for (int i = 0; i < 2; ++i) {
+        if (c->st_done[i]) (void)hipEventDestroy(c->st_done[i]);
+        if (c->st_copied[i]) (void)hipEventDestroy(c->st_copied[i]);
+    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PFAAI_OK;
@@ -440,8 +474,10 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     if (p.mode < 0 || p.mode > 2) return fail(c, PFAAI_ERR_INVALID, "mode must be 0, 1 or 2");
     if (p.n_ids < 2 || p.n_prot < 1 || p.n_prot >= kMaxRuns || p.t_cols < 1)
         return fail(c, PFAAI_ERR_INVALID, "bad sizes (n_ids >= 2, 1 <= n_prot < 4096)");
-    if (p.n_ids >= (1 << 21) || p.n_f < 0 || p.n_f >= (int64_t)1 << 31)
-        return fail(c, PFAAI_ERR_INVALID, "n_ids must be < 2^21 and |F| < 2^31");
+    // 21-bit genome ids (run-table splitters, first-key packing); F indices
+    // are u32 in the run table / work lists (and 16-B records in k_rows_pl)
+    if (p.n_ids >= (1 << 21) || p.n_f < 0 || p.n_f > kMaxF)
+        return fail(c, PFAAI_ERR_INVALID, "n_ids must be < 2^21 and |F| <= 2^32 - 64");
     if (!p.Lp || !p.F_prot || !p.F_genome || !p.T)
         return fail(c, PFAAI_ERR_INVALID, "Lp, F_prot, F_genome and T are required");
     if (p.Lp[0] != 0 || p.Lp[PFAAI_NTETRAMERS] != p.n_f)
@@ -458,6 +494,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         if (p.T[i] < 0 || p.T[i] > 65535) return fail(c, PFAAI_ERR_INVALID, "T entries must lie in [0, 65535]");
 
     c->prob = p;
+    c->runs_valid = c->runs_key = false;
     const int32_t ni = p.n_ids;
     // output rows and derived maps
     std::vector<int32_t> row_of(ni, -1), tcol_row(ni), tcol_col(ni);
@@ -892,6 +929,119 @@ int pfaai_synchronize(pfaai_ctx* c) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipDeviceSynchronize());
+    return PFAAI_OK;
+}
+
+
+// Output-tile streaming (config C5, a matrix too large to
+// hold whole on the host or the device).  Rows are cut into tiles of at most
+// tile_pairs JAC entries; tile k is computed into device buffer k & 1 on the
+// context stream while tile k - 1 is copied to pinned host buffer (k-1) & 1
+// on the copy stream and tile k - 2 is handed to the sink on this thread.
+// The run table is built by the first tile only (PFAAI_FLAG_KEEP_RUNS).
+int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,
+                 void* user) {
+    if (!c) return PFAAI_ERR_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    if (!sink) return fail(c, PFAAI_ERR_INVALID, "sink is required");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
+    if (c->prob.mode == PFAAI_MODE_QSUB)
+        return fail(c, PFAAI_ERR_INVALID, "pfaai_stream: QSUB rows have no contiguous JAC span (use pfaai_run)");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool jac = flags & PFAAI_FLAG_EMIT_JAC;
+    c->st_events = 0;
+    if (rb == re) return PFAAI_OK;
+    // row tiles: maximal row ranges whose span fits tile_pairs (>= one row)
+    std::vector<int64_t> cut{rb};
+    int64_t cap = 1;
+    for (int64_t r = rb; r < re;) {
+        int64_t f0, n0, r2 = r + 1;
+        pfaai_row_span(c, r, r2, &f0, &n0);
+        while (r2 < re) {
+            int64_t f1, n1;
+            pfaai_row_span(c, r, r2 + 1, &f1, &n1);
+            if (n1 > tile_pairs) break;
+            n0 = n1;
+            ++r2;
+        }
+        cap = std::max(cap, n0);
+        cut.push_back(r2);
+        r = r2;
+    }
+    const int64_t ntiles = (int64_t)cut.size() - 1;
+    const size_t per = (size_t)cap * (sizeof(double) + (jac ? sizeof(double) + sizeof(int32_t) : 0));
+    int rc;
+    if ((rc = ensure(c, c->st_dev, 2 * per))) return rc;
+    const size_t host_bytes = 2 * per + (size_t)ntiles * sizeof(unsigned long long);
+    if (c->st_host_bytes < host_bytes) {
+        if (c->st_host) (void)hipHostFree(c->st_host);
+        c->st_host = nullptr;
+        c->st_host_bytes = 0;
+        HIPCHK(c, hipHostMalloc(&c->st_host, host_bytes, hipHostMallocDefault));
+        c->st_host_bytes = host_bytes;
+    }
+    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        if (!c->st_done[i]) HIPCHK(c, hipEventCreateWithFlags(&c->st_done[i], hipEventDisableTiming));
+        if (!c->st_copied[i]) HIPCHK(c, hipEventCreateWithFlags(&c->st_copied[i], hipEventDisableTiming));
+    }
+    auto dptr = [&](int b, int which) -> char* {  // 0 aji, 1 S, 2 N of device buffer b
+        char* base = static_cast<char*>(c->st_dev.p) + b * per;
+        return base + (which == 0 ? 0 : which == 1 ? cap * sizeof(double) : 2 * cap * sizeof(double));
+    };
+    auto hptr = [&](int b, int which) -> char* {
+        char* base = static_cast<char*>(c->st_host) + b * per;
+        return base + (which == 0 ? 0 : which == 1 ? cap * sizeof(double) : 2 * cap * sizeof(double));
+    };
+    auto* evs = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->st_host) + 2 * per);
+    const auto* sc_ev = static_cast<unsigned long long*>(c->scalars.p) + SC_EVENTS;
+    auto drain = [&]() {  // error exit: nothing may still write the buffers
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->copy_stream);
+    };
+    auto deliver = [&](int64_t k) -> int {
+        const int b = (int)(k & 1);
+        HIPCHK(c, hipEventSynchronize(c->st_copied[b]));
+        int64_t f, n;
+        pfaai_row_span(c, cut[k], cut[k + 1], &f, &n);
+        c->st_events += (int64_t)evs[k];
+        const int src = sink(user, cut[k], cut[k + 1], f, n, reinterpret_cast<const double*>(hptr(b, 0)),
+                             jac ? reinterpret_cast<const double*>(hptr(b, 1)) : nullptr,
+                             jac ? reinterpret_cast<const int32_t*>(hptr(b, 2)) : nullptr);
+        return src ? fail(c, src, "pfaai_stream: the sink stopped the stream") : PFAAI_OK;
+    };
+    for (int64_t k = 0; k < ntiles; ++k) {
+        const int b = (int)(k & 1);
+        int64_t f, n;
+        pfaai_row_span(c, cut[k], cut[k + 1], &f, &n);
+        if (k >= 2) {  // host buffer b is reused below: hand tile k - 2 over first
+            if ((rc = deliver(k - 2))) { drain(); return rc; }
+        }
+        // device buffer b was last read by the copy of tile k - 2
+        if (k >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, c->st_copied[b], 0));
+        auto* aji = reinterpret_cast<double*>(dptr(b, 0)) - f;  // kernels index by the global JAC index
+        auto* S = jac ? reinterpret_cast<double*>(dptr(b, 1)) - f : nullptr;
+        auto* N = jac ? reinterpret_cast<int32_t*>(dptr(b, 2)) - f : nullptr;
+        rc = pfaai_run(c, cut[k], cut[k + 1], flags | (k ? PFAAI_FLAG_KEEP_RUNS : 0u), aji, S, N, c->stream);
+        if (rc) { drain(); return rc; }
+        HIPCHK(c, hipMemcpyAsync(&evs[k], sc_ev, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->st_done[b], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->st_done[b], 0));
+        HIPCHK(c, hipMemcpyAsync(hptr(b, 0), dptr(b, 0), n * sizeof(double), hipMemcpyDeviceToHost, c->copy_stream));
+        if (jac) {
+            HIPCHK(c, hipMemcpyAsync(hptr(b, 1), dptr(b, 1), n * sizeof(double), hipMemcpyDeviceToHost, c->copy_stream));
+            HIPCHK(c, hipMemcpyAsync(hptr(b, 2), dptr(b, 2), n * sizeof(int32_t), hipMemcpyDeviceToHost, c->copy_stream));
+        }
+        HIPCHK(c, hipEventRecord(c->st_copied[b], c->copy_stream));
+    }
+    for (int64_t k = std::max<int64_t>(0, ntiles - 2); k < ntiles; ++k)
+        if ((rc = deliver(k))) { drain(); return rc; }
+    return PFAAI_OK;
+}
+
+int pfaai_stream_events(const pfaai_ctx* c, int64_t* n_events) {
+    if (!c || !n_events) return PFAAI_ERR_INVALID;
+    *n_events = c->st_events;
     return PFAAI_OK;
 }
 

@@ -70,9 +70,12 @@ __device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint3
 // Member loads of line task k of this lane's 4-lane group: 4 members (16 B)
 // of the task's 64-B line, issued unconditionally (an out-of-range offset
 // where the lane has none).  Bit j of the result: member j of b is valid.
-template <int TC = kPlTaskCap>
-__device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, const uint2* rt, int k, int nt, int gl,
-                                             uint4& b) {
+// BIGF (|F| >= 2^30, where a 32-bit byte offset into F wraps -- buffer
+// offsets, strided index included, are 32-bit on gfx9): a 64-bit global load
+// instead; a lane without members re-reads F[0..3] (its ok bits are clear).
+template <int TC = kPlTaskCap, bool BIGF = false>
+__device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
+                                             const uint2* rt, int k, int nt, int gl, uint4& b) {
     const uint32_t t = tk[min(k, TC - 1)];
     const uint2 rr = rt[t & 1023u];
     const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + (t >> 10) * kGroup + 4u * (uint32_t)gl;
@@ -80,7 +83,10 @@ __device__ __forceinline__ uint32_t pl_issue(rsrc_t fg, const uint16_t* tk, cons
     uint32_t ok = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) ok |= (uint32_t)(task && m0 + j >= rr.x && m0 + j < rr.y) << j;
-    b = bld_u128(fg, ok ? m0 * 4u : kOOB, 0u);
+    if constexpr (BIGF)
+        b = *reinterpret_cast<const uint4*>(Fg + (ok ? m0 : 0u));
+    else
+        b = bld_u128(fg, ok ? m0 * 4u : kOOB, 0u);
     return ok;
 }
 
@@ -101,7 +107,7 @@ constexpr int kClkBlocks = 256;
 
 // NL: the per-column counts N live in LDS (u8 pairs, P <= 255) instead of
 // registers -- 5 VGPRs less at KW = 5, paid for with half the task capacity.
-template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false>
+template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
                                                    double* __restrict__ aji, double* __restrict__ s_out,
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // S4a: first round of member loads of protein i (one task per 4-lane group)
         const int nt = has_i ? min((int)uni_u32(ntask[cs]), TC) : 0;
         uint4 b;
-        uint32_t okm = pl_issue<TC>(r_fg, tk[st], rt[st], grp, nt, gl, b);
+        uint32_t okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], grp, nt, gl, b);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
         if (i + 1 < P) s3(i + 1, r4);
@@ -303,13 +309,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             int k = grp + NG;
             for (; k + NG < nt; k += 2 * NG) {
                 uint4 b2;
-                okm = pl_issue<TC>(r_fg, tk[st], rt[st], k, nt, gl, b);
-                const uint32_t ok2 = pl_issue<TC>(r_fg, tk[st], rt[st], k + NG, nt, gl, b2);
+                okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k, nt, gl, b);
+                const uint32_t ok2 = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k + NG, nt, gl, b2);
                 pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
                 pl_scatter4<MODE>(d, a, b2, ok2, acc_i, cc0, wlo, whi);
             }
             if (k < nt) {
-                okm = pl_issue<TC>(r_fg, tk[st], rt[st], k, nt, gl, b);
+                okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k, nt, gl, b);
                 pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
             }
             if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                         m &= m - 1u;
                         const uint32_t rx = uni_u32(rt[st][wd * 32 + s].x), ry = uni_u32(rt[st][wd * 32 + s].y);
                         for (uint32_t mm = rx + tid; mm < ry; mm += NT)
-                            pl_add<MODE>(d, a, (int32_t)bld_u32(r_fg, mm * 4u, 0u), acc_i, cc0, wlo, whi);
+                            pl_add<MODE>(d, a, d.Fg[mm], acc_i, cc0, wlo, whi);
                     }
                 }
             }

@@ -40,6 +40,8 @@ struct AppParams {  // main.cpp:56-131
     int device = 0;
     std::string dumpPrefix;    // --dump-arrays: write the loader's Lc/F/T (cereal) and exit (no GPU)
     std::string formatSelftest;  // --format-selftest FILE: print fmt-formatted doubles (hex input)
+    std::string streamAji;       // --stream-aji FILE: pfaai_stream the AJI vector to FILE (no CSV)
+    long long tilePairs = 1ll << 27;
 
     void print() const {
         std::vector<std::string> args = {" Input Database  : " + pathToDatabase + " ",
@@ -81,7 +83,10 @@ const char* kUsage =
     "  -q,--query_subset TEXT:FILE  Path to Query List (Should be subset of genomoes in the input DB.)\n"
     "  --ref-compat             Reproduce the reference's quirks (zero-overlap pairs, QT T indexing)\n"
     "  --device INT [0]         HIP device\n"
-    "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n";
+    "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n"
+    "  --stream-aji TEXT        Stream the AJI vector (JAC-index order, cereal vector<double>) to FILE\n"
+    "                           tile by tile instead of writing the CSV matrix (-q not supported)\n"
+    "  --tile-pairs INT [134217728]  Pairs per streamed output tile\n";
 
 // CLI11-compatible parse: returns -1 to continue, else the exit code.
 int parse(int argc, char** argv, AppParams& a) {
@@ -116,6 +121,13 @@ int parse(int argc, char** argv, AppParams& a) {
             std::string v;
             if (!value(v)) return 114;
             a.device = std::atoi(v.c_str());
+        } else if (is("--stream-aji", "--stream-aji")) {
+            if (!value(a.streamAji)) return 114;
+        } else if (is("--tile-pairs", "--tile-pairs")) {
+            std::string v;
+            if (!value(v)) return 114;
+            a.tilePairs = std::atoll(v.c_str());
+            if (a.tilePairs < 1) return 105;
         } else if (is("--bin", "--bin")) {
             if (!value(a.binPrefix)) return 114;
         } else if (is("--dump-arrays", "--dump-arrays")) {
@@ -191,6 +203,16 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
     auto t0 = std::chrono::steady_clock::now();
     try {
         pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, app.device, app.refCompat);
+        if (!app.streamAji.empty()) {  // output-tile streaming: no CSV, no whole matrix anywhere
+            if (mode == PFAAI_MODE_QSUB) {
+                std::cerr << "--stream-aji does not support -q" << std::endl;
+                return PFAAI_ERR_INVALID;
+            }
+            int rc = impl.streamAJI(app.streamAji, app.tilePairs);
+            std::printf("AJI stream (MI355X) : %10.2f ms  (|E| = %lld) -> %s\n", ms_since(t0),
+                        (long long)impl.nEvents(), app.streamAji.c_str());
+            return rc;
+        }
         impl.run();
         std::printf("AJI (MI355X)        : %10.2f ms  (|E| = %lld; work lists %.2f ms, rows %.2f ms)\n",
                     ms_since(t0), (long long)impl.nEvents(), impl.msBuild(), impl.msRows());

@@ -24,20 +24,27 @@ def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: flo
     """-> [(row_begin, row_end)] * world, contiguous, covering [0, n_rows),
     balanced by the row cost model fixed_cols + width (all-vs-all row a has
     width n-1-a; QT/QSUB rows are equal)."""
+    return split_range(0, n_rows, world, n_rows, all_vs_all, fixed_cols)
+
+
+def split_range(row_lo: int, row_hi: int, parts: int, n_rows: int, all_vs_all: bool = True,
+                fixed_cols: float | None = None):
+    """split_rows for the sub-range [row_lo, row_hi) of an n_rows matrix
+    (e.g. a rank's block cut into pipeline chunks)."""
     if not all_vs_all:
-        cuts = [n_rows * r // world for r in range(world + 1)]
-        return [(cuts[i], cuts[i + 1]) for i in range(world)]
+        cuts = [row_lo + (row_hi - row_lo) * r // parts for r in range(parts + 1)]
+        return [(cuts[i], cuts[i + 1]) for i in range(parts)]
     n = n_rows
     k = FIXED_COST_FRACTION * n if fixed_cols is None else float(fixed_cols)
 
     def before(a):  # cost of rows < a: a fixed parts + the pairs of the upper triangle
         return a * k + a * n - a * (a + 1) // 2
 
-    total = before(n)
-    cuts = [0]
-    for r in range(1, world):
-        target = total * r / world
-        lo, hi = cuts[-1], n
+    c0, c1 = before(row_lo), before(row_hi)
+    cuts = [row_lo]
+    for r in range(1, parts):
+        target = c0 + (c1 - c0) * r / parts
+        lo, hi = cuts[-1], row_hi
         while lo < hi:
             mid = (lo + hi) // 2
             if before(mid) < target:
@@ -45,8 +52,62 @@ def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: flo
             else:
                 hi = mid
         cuts.append(lo)
-    cuts.append(n)
-    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+    cuts.append(row_hi)
+    return [(cuts[i], cuts[i + 1]) for i in range(parts)]
+
+
+class PipelinedGather:
+    """Row blocks cut into `chunks` pipeline chunks per rank.  Chunk j of every
+    rank has its own buffer (padded to the largest rank's chunk j); issue(j)
+    starts an asynchronous gather of it to `dst` as soon as it is computed,
+    so the transfer of chunk j over xGMI overlaps the computation of chunk
+    j + 1 (RCCL runs on its own stream, ordered after the work already on
+    the current stream when issue() is called).
+
+    counts[r][j]: JAC entries of rank r's chunk j.  Because rank blocks and
+    their chunks are contiguous row ranges in row order, and rows map to
+    contiguous, increasing JAC spans (all-vs-all, QT), the concatenation
+    over (r, j) of the received chunks is the full JAC-ordered vector."""
+
+    def __init__(self, counts, dst=0, device=None, dtype=None, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dst = dst
+        self.counts = counts
+        nchunks = len(counts[0])
+        dtype = dtype or torch.float64
+        self.bufs = [torch.zeros(max(1, max(c[j] for c in counts)), dtype=dtype, device=device)
+                     for j in range(nchunks)]
+        self.recv = ([[torch.empty_like(b) for _ in range(self.world)] for b in self.bufs]
+                     if (self.world > 1 and self.rank == dst) else None)
+        self.works = []
+
+    def issue(self, j):
+        if self.world == 1:
+            return
+        self.works.append(self.dist.gather(self.bufs[j], self.recv[j] if self.recv else None, dst=self.dst,
+                                           group=self.group, async_op=True))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+    def result(self):
+        """The full vector on dst (after wait()), None elsewhere."""
+        import torch
+
+        if self.world == 1:
+            return torch.cat([b[: self.counts[0][j]] for j, b in enumerate(self.bufs)])
+        if self.rank != self.dst:
+            return None
+        return torch.cat([self.recv[j][r][: self.counts[r][j]]
+                          for r in range(self.world) for j in range(len(self.bufs))])
 
 
 def gather_rows(out_local, counts, dst=0, group=None):

@@ -86,3 +86,55 @@ def test_gloo_world2_gather_equals_single():
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=10) is True
+
+
+def _pipe_worker(rank, world, port, n, chunks, result_q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from parfastaai_amd.shard import PipelinedGather, split_range, split_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    base = lambda a: n * a - a * (a + 1) // 2  # JAC index of (a, a+1), ds_impl.hpp:83-86  # noqa: E731
+    blocks = split_rows(n, world)
+    sub = [split_range(b0, b1, chunks, n) for b0, b1 in blocks]
+    counts = [[base(c1) - base(c0) for c0, c1 in s] for s in sub]
+    pg = PipelinedGather(counts, dst=0)
+    for j, (c0, c1) in enumerate(sub[rank]):  # "compute" chunk j: its JAC indices
+        pg.bufs[j][: counts[rank][j]] = torch.arange(base(c0), base(c1), dtype=torch.float64)
+        pg.issue(j)
+    pg.wait()
+    full = pg.result()
+    if rank == 0:
+        result_q.put(bool(torch.equal(full, torch.arange(n * (n - 1) // 2, dtype=torch.float64))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 1)])
+def test_gloo_pipelined_gather_covers_jac_order(world, chunks):
+    """bench.py's N > 1 step: rank blocks cut into pipeline chunks, each chunk
+    gathered asynchronously as soon as it is computed; rank 0's concatenation
+    is the full JAC-ordered vector."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, 157, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True
+
+
+def test_split_range_chunks():
+    from parfastaai_amd.shard import split_range
+
+    n = 10000
+    for b0, b1 in split_rows(n, 8):
+        sub = split_range(b0, b1, 4, n)
+        assert sub[0][0] == b0 and sub[-1][1] == b1
+        assert all(sub[i][1] == sub[i + 1][0] for i in range(3))
+    assert split_range(10, 20, 3, 100, all_vs_all=False) == [(10, 13), (13, 16), (16, 20)]

@@ -91,3 +91,22 @@ def test_cli_vs_reference_binary_on_syn(tmp_path, case):
                      n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
         run(tdb, out, "-r", qdb, "--ref-compat")
     assert open(out).read() == text(f"ref_{case}.csv")
+
+
+@pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
+def test_cli_stream_aji_equals_reference_bin(tmp_path, name):
+    """--stream-aji (pfaai_stream, tiles of 7 pairs) writes the reference's
+    own <prefix>_aji.bin bytes."""
+    db = unpack(tmp_path, name + ".db")
+    out = tmp_path / "s_aji.bin"
+    run(db, str(tmp_path / "unused.csv"), "--stream-aji", str(out), "--tile-pairs", "7")
+    assert np.array_equal(fm.read_vec_f64(str(out)), fm.read_vec_f64(gpath(name + "_aji.bin")))
+    assert not (tmp_path / "unused.csv").exists()
+
+
+def test_cli_stream_aji_qt_ref_compat(tmp_path):
+    t = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    out = tmp_path / "s_aji.bin"
+    run(t, str(tmp_path / "unused.csv"), "-r", q, "--ref-compat", "--stream-aji", str(out), "--tile-pairs", "50")
+    assert np.array_equal(fm.read_vec_f64(str(out)), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))

@@ -1,0 +1,128 @@
+"""Output-tile streaming (pfaai_stream), the
+run-table reuse flag (PFAAI_FLAG_KEEP_RUNS) and F past 2^30 entries (where a
+32-bit byte offset into F wraps), all through the C ABI on the GPU, bit-exact
+against pfaai_compute and the CPU oracle."""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import qt_syn
+from parfastaai_amd import _capi, syn
+from parfastaai_amd.datastruct import ParFAAIData, ParFAAIQSubData
+
+pytestmark = pytest.mark.gpu
+
+
+def _all_problem(n, p, **kw):
+    g = syn.generate(n, p, **kw)
+    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    return ds.with_genome_major(g["G_off"], g["G_tet"]).problem()
+
+
+def _collect(engine, rb, re, tile, flags):
+    """-> (aji, S, N) over the rows' JAC span, tiles checked to arrive in order."""
+    f0, cnt = engine.row_span(rb, re)
+    aji = np.full(cnt, np.nan)
+    S = np.full(cnt, np.nan)
+    N = np.full(cnt, -1, np.int32)
+    seen = []
+
+    def sink(r0, r1, first, a, s, n):
+        assert not seen or seen[-1][1] == r0, "tiles out of order"
+        assert len(a) <= max(tile, engine.row_span(r0, r0 + 1)[1])
+        seen.append((r0, r1))
+        aji[first - f0: first - f0 + len(a)] = a
+        if s is not None:
+            S[first - f0: first - f0 + len(a)] = s
+            N[first - f0: first - f0 + len(a)] = n
+        return 0
+
+    ne = engine.stream(rb, re, tile, flags, sink)
+    assert seen[0][0] == rb and seen[-1][1] == re
+    return aji, S, N, ne, len(seen)
+
+
+@pytest.mark.parametrize("compat", [False, True], ids=["default", "ref-compat"])
+def test_stream_all_equals_compute(engine, compat):
+    pb = _all_problem(300, 30, clade_size=10)
+    engine.load(**pb)
+    flags = _capi.FLAG_REF_COMPAT if compat else 0
+    aji, S, N = engine.compute(flags)
+    # tiles of <= 997 pairs: ~45 tiles, the last rows several per tile
+    a2, S2, N2, ne, nt = _collect(engine, 0, 300, 997, flags | _capi.FLAG_EMIT_JAC)
+    assert nt > 20
+    assert np.array_equal(a2, aji) and np.array_equal(S2, S) and np.array_equal(N2, N)
+    assert ne == O.Problem(pb, compat=compat).count_e()
+    # AJI only (no S/N), a row sub-range
+    f0, cnt = engine.row_span(40, 211)
+    a3, S3, _, _, _ = _collect(engine, 40, 211, 5000, flags)
+    assert np.array_equal(a3, aji[f0:f0 + cnt]) and np.isnan(S3).all()
+
+
+def test_stream_qt_equals_compute(engine):
+    ds = qt_syn(dict(n_tgt=60, n_qry=25, n_prot=20, clade_size=6), genome_major=True)
+    engine.load(**ds.problem())
+    aji, S, N = engine.compute(0)
+    a2, S2, N2, _, nt = _collect(engine, 0, 25, 130, _capi.FLAG_EMIT_JAC)
+    assert nt == 13  # two 60-column rows per tile
+    assert np.array_equal(a2, aji) and np.array_equal(S2, S) and np.array_equal(N2, N)
+
+
+def test_stream_rejects_qsub_and_sink_stop(engine):
+    pb = _all_problem(80, 10, clade_size=8)
+    engine.load(**pb)
+    calls = []
+    with pytest.raises(_capi.PfaaiError) as ei:
+        engine.stream(0, 80, 100, 0, lambda *a: calls.append(a[0]) or len(calls) == 2)
+    assert ei.value.code == 7 and len(calls) == 2
+    g = syn.generate(30, 5, clade_size=5)
+    q = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"],
+                                   [g["genome_set"][i] for i in (3, 9, 17)])
+    engine.load(**q.problem())
+    with pytest.raises(_capi.PfaaiError):
+        engine.stream(0, 3, 100, 0, lambda *a: 0)
+
+
+def test_keep_runs_matches_single_run(engine):
+    """Rows computed in three pfaai_run calls, the later two reusing the run
+    table, equal one run over all rows."""
+    import torch
+
+    pb = _all_problem(500, 40, clade_size=12)
+    engine.load(**pb)
+    aji, _, _ = engine.compute(0)
+    _, npairs = engine.shape()
+    out = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for i, (rb, re) in enumerate([(0, 90), (90, 301), (301, 500)]):
+        engine.run(rb, re, _capi.FLAG_KEEP_RUNS if i else 0, out.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), aji)
+    n_runs, ms_build, _ = engine.timing(reset=True)
+    assert n_runs >= 3
+
+
+@pytest.mark.timeout(600)
+def test_f_beyond_2_30_entries(engine):
+    """|F| > 2^30: member ids past byte offset 2^32 of F (SYN N = 38 000,
+    |F| ~ 1.09e9); sampled rows streamed and checked against the oracle's
+    dense restatement, |E| of those rows included."""
+    n = 38000
+    g = syn.generate(n, 100)
+    nf = len(g["F_genome"])
+    assert nf > (1 << 30), nf
+    pb = dict(mode=_capi.MODE_ALL, n_ids=n, n_prot=100, Lp=g["Lp"], F_prot=g["F_prot"],
+              F_genome=g["F_genome"], T=g["T"], G_off=g["G_off"], G_tet=g["G_tet"])
+    engine.load(**pb)
+    del g
+    pr = O.Problem(pb)
+    for lo, hi in [(0, 2), (20011, 20013), (n - 40, n - 37)]:
+        f0, _ = engine.row_span(lo, hi)
+        aji, S, N, ne, _ = _collect(engine, lo, hi, 1 << 20, _capi.FLAG_EMIT_JAC)
+        So, No, neo = pr.dense_rows(lo, hi)
+        assert ne == neo
+        for a in range(lo, hi):
+            b = np.arange(a + 1, n)
+            k = n * a + b - (a + 2) * (a + 1) // 2 - f0
+            assert np.array_equal(S[k], So[a - lo, b]) and np.array_equal(N[k], No[a - lo, b])
+            assert np.array_equal(aji[k], np.where(N[k] > 0, S[k] / np.maximum(N[k], 1), 0.0))
