@@ -124,8 +124,10 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=320)
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="N > 1: pipeline chunks per rank (gather of chunk j overlaps chunk j+1)")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="pipeline chunks per rank (gather of chunk j overlaps chunk j+1); "
+                         "default 1 at N = 1, 2 at N > 1 (tools/gpu/shard_times.py: 4 chunks add "
+                         "0.95 ms of launch tails per 10k/8 shard, 2 chunks 0.25 ms)")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     args = ap.parse_args()
@@ -164,7 +166,7 @@ def main():
     # N > 1: the rank's rows in pipeline chunks; chunk j's AJI is gathered to
     # rank 0 (RCCL, async) while chunk j+1 computes; the run table is built
     # by chunk 0 only (PFAAI_FLAG_KEEP_RUNS)
-    nch = 1 if world == 1 else max(1, args.chunks)
+    nch = max(1, args.chunks) if args.chunks else (1 if world == 1 else 2)
     sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
     counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
     pg = PipelinedGather(counts, dst=0, device=dev)

@@ -133,3 +133,27 @@ def write_db(path, n_genomes, n_prot=100, genome_prefix="syn", **kw) -> dict:
     con.close()
     g["genome_set"] = gnames
     return g
+
+
+def qt_merge(gt: dict, gq: dict) -> dict:
+    """QT problem arrays from a target and a query SYN DB (generate() dicts)
+    joined as the reference's QT loader does (scp_db.hpp:450-528): per
+    (tetramer, protein) block present in both, target genomes then query
+    genomes + n_tgt; T side by side; the genome-major lists concatenated
+    (entries whose block is absent from F are ignored by the engine).  The
+    linear C merge of tools/syn_gen.c (tests/helpers.py:qt_syn is the numpy
+    statement of the same join)."""
+    L = _load()
+    vp = ctypes.c_void_p
+    L.syn_qt_merge.restype = ctypes.c_int64
+    L.syn_qt_merge.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_int32, vp, vp, vp]
+    nT = gt["T"].shape[1]
+    Lp = np.zeros(NTETRAMERS + 1, dtype=np.int64)
+    args = [_p(gt["Lp"]), _p(gt["F_prot"]), _p(gt["F_genome"]), _p(gq["Lp"]), _p(gq["F_prot"]), _p(gq["F_genome"]), nT]
+    n = L.syn_qt_merge(*args, _p(Lp), None, None)
+    Fp = np.empty(max(n, 1), dtype=np.int32)
+    Fg = np.empty(max(n, 1), dtype=np.int32)
+    L.syn_qt_merge(*args, _p(Lp), _p(Fp), _p(Fg))
+    G_off = np.concatenate([gt["G_off"], gq["G_off"][1:] + gt["G_off"][-1]])
+    return dict(Lp=Lp, F_prot=Fp[:n], F_genome=Fg[:n], T=np.concatenate([gt["T"], gq["T"]], axis=1),
+                G_off=G_off, G_tet=np.concatenate([gt["G_tet"], gq["G_tet"]]), n_tgt=nT, n_qry=gq["T"].shape[1])

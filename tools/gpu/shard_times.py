@@ -34,4 +34,22 @@ for label, kw in (("cost model", {}), ("pair balance", {"fixed_cols": 0})):
         ms.append(float(np.median(t)))
     print(f"{label:12s} rows/shard {[b1 - b0 for b0, b1 in blocks]}")
     print(f"{label:12s} k_rows ms  {[round(x, 3) for x in ms]}  max {max(ms):.3f}  mean {np.mean(ms):.3f}")
+
+# bench.py's pipeline chunks: a rank's block as 1, 2 or 4 k_rows launches
+# (run table reused) -- the launch-tail cost of chunking the gather pipeline
+from parfastaai_amd.shard import split_range  # noqa: E402
+
+blocks = split_rows(rows, world)
+for nch in (1, 2, 4):
+    ms = []
+    for rb, re_ in blocks:
+        t = []
+        for _ in range(3):
+            eng.timing(reset=True)
+            for j, (c0, c1) in enumerate(split_range(rb, re_, nch, rows)):
+                eng.run(c0, c1, _capi.FLAG_KEEP_RUNS if j else 0, d)
+            _, b, r = eng.timing(reset=True)
+            t.append(b + r)
+        ms.append(float(np.median(t)))
+    print(f"chunks {nch}: k_blk + k_rows ms per shard {[round(x, 3) for x in ms]}  max {max(ms):.3f}")
 eng.free(d)

@@ -199,3 +199,42 @@ int32_t syn_genome_set(const syn_params* p, int32_t g, int32_t prot, int32_t* ou
     int32_t na = ancestral(p, clade_of(p, g) % C, prot, anc);
     return genome_set(p, g, prot, anc, na, out);
 }
+
+/*
+ * QT join of two F arrays (both ordered by (tetramer, protein, genome)), as
+ * the reference's query-vs-target loader builds it (scp_db.hpp:450-528): for
+ * every (tetramer, protein) block present in BOTH, the target genomes then
+ * the query genomes offset by n_tgt.  Lp_out[NTET + 1]; Fp_out / Fg_out may
+ * be NULL (count only).  Returns |F_out|.
+ */
+int64_t syn_qt_merge(const int64_t* Lpt, const int32_t* Fpt, const int32_t* Fgt, const int64_t* Lpq,
+                     const int32_t* Fpq, const int32_t* Fgq, int32_t n_tgt, int64_t* Lp_out, int32_t* Fp_out,
+                     int32_t* Fg_out) {
+    int64_t o = 0;
+    Lp_out[0] = 0;
+    for (int32_t t = 0; t < NTET; t++) {
+        int64_t i = Lpt[t], ie = Lpt[t + 1], j = Lpq[t], je = Lpq[t + 1];
+        while (i < ie && j < je) {
+            const int32_t pt = Fpt[i], pq = Fpq[j];
+            int64_t i2 = i, j2 = j;
+            while (i2 < ie && Fpt[i2] == pt) i2++;
+            while (j2 < je && Fpq[j2] == pq) j2++;
+            if (pt == pq) {
+                if (Fp_out) {
+                    for (int64_t k = i; k < i2; k++, o++) { Fp_out[o] = pt; Fg_out[o] = Fgt[k]; }
+                    for (int64_t k = j; k < j2; k++, o++) { Fp_out[o] = pq; Fg_out[o] = Fgq[k] + n_tgt; }
+                } else {
+                    o += (i2 - i) + (j2 - j);
+                }
+                i = i2;
+                j = j2;
+            } else if (pt < pq) {
+                i = i2;
+            } else {
+                j = j2;
+            }
+        }
+        Lp_out[t + 1] = o;
+    }
+    return o;
+}
