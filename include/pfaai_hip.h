@@ -103,6 +103,21 @@ const char* pfaai_last_error(const pfaai_ctx* ctx);
  * 75-79).  Replaces any previously loaded problem. */
 int pfaai_load(pfaai_ctx* ctx, const pfaai_problem* prob);
 
+/* F construction on the device (replaces DataStructHelper::constructLc /
+ * constructF / constructT, ds_helper.hpp:46-162, and the SQL UNION ALL +
+ * ORDER BY of SQLiteSCPDataBase::proteinSetGPPairs, scp_db.hpp:161-216).
+ * Input: n (protein, genome, tetramer) triples -- the `<p>_genomes` blobs
+ * expanded -- where each protein's triples come in non-decreasing genome
+ * order (any (genome, protein)- or (protein, genome)-major walk of the blobs).
+ * A stable LSD radix sort (8-bit digits) by tetramer * n_prot + protein
+ * yields F ordered by (tetramer, protein, genome).  Outputs (host, caller-
+ * allocated): Lc[160000], Lp[160001], F_prot / F_genome[n], and optionally
+ * T[n_prot * n_genome] (counts per (protein, genome); NULL to skip).  Does
+ * not change the loaded problem. */
+int pfaai_build_f(pfaai_ctx* ctx, const int32_t* prot, const int32_t* genome, const int32_t* tetra,
+                  int64_t n, int32_t n_prot, int32_t n_genome, int32_t* Lc_out, int64_t* Lp_out,
+                  int32_t* F_prot_out, int32_t* F_genome_out, int32_t* T_out);
+
 /* Number of output rows (ALL: n_ids; QSUB/QT: n_qry) and of JAC pairs
  * (nGenomePairs: ds_impl.hpp:78-80, 244-249, 406). */
 int pfaai_shape(const pfaai_ctx* ctx, int64_t* n_rows, int64_t* n_pairs);

@@ -33,6 +33,7 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
+    "pfaai_build_f",
 ]
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
@@ -90,6 +91,7 @@ def load_library():
         "pfaai_device_free": (ctypes.c_int, [vp, vp]),
         "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
         "pfaai_synchronize": (ctypes.c_int, [vp]),
+        "pfaai_build_f": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
@@ -178,6 +180,25 @@ class Engine:
         """Device-resident run; d_* are device pointers (ints), stream a hipStream_t (int)."""
         self._check(self.lib.pfaai_run(self.ctx, row_begin, row_end, flags, d_aji, d_S, d_N, stream),
                     "pfaai_run")
+
+    def build_f(self, prot, genome, tetra, n_prot, n_genome, with_T=True):
+        """F construction on the device (pfaai_build_f) from (protein, genome,
+        tetramer) triples, each protein's in non-decreasing genome order ->
+        dict(Lc int32[160000], Lp int64[160001], F_prot, F_genome int32[n],
+        T int32[n_prot, n_genome] or None), F by (tetramer, protein, genome)."""
+        prot = np.ascontiguousarray(prot, dtype=np.int32)
+        genome = np.ascontiguousarray(genome, dtype=np.int32)
+        tetra = np.ascontiguousarray(tetra, dtype=np.int32)
+        n = prot.shape[0]
+        assert genome.shape == (n,) and tetra.shape == (n,)
+        Lc = np.zeros(NTETRAMERS, dtype=np.int32)
+        Lp = np.zeros(NTETRAMERS + 1, dtype=np.int64)
+        Fp = np.empty(max(n, 1), dtype=np.int32)
+        Fg = np.empty(max(n, 1), dtype=np.int32)
+        T = np.zeros((n_prot, n_genome), dtype=np.int32) if with_T else None
+        self._check(self.lib.pfaai_build_f(self.ctx, _ptr(prot), _ptr(genome), _ptr(tetra), n, n_prot, n_genome,
+                                           _ptr(Lc), _ptr(Lp), _ptr(Fp), _ptr(Fg), _ptr(T)), "pfaai_build_f")
+        return dict(Lc=Lc, Lp=Lp, F_prot=Fp[:n], F_genome=Fg[:n], T=T)
 
     def stream(self, row_begin, row_end, tile_pairs, flags, sink):
         """Output-tile streaming (pfaai_stream): sink(row_begin, row_end, first,

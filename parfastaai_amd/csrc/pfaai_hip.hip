@@ -1045,4 +1045,114 @@ int pfaai_stream_events(const pfaai_ctx* c, int64_t* n_events) {
     return PFAAI_OK;
 }
 
+
+// F construction on the device (SURVEY 8b pfaai_build_f; ds_helper.hpp:82-162,
+// scp_db.hpp:161-262): count Lc / T, stable LSD radix sort of the triples by
+// tetramer * P + protein (8-bit digits, the work-list sort's kernels), split
+// the sorted (protein, genome) records into the F columns.
+int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, const int32_t* tetra, int64_t n,
+                  int32_t n_prot, int32_t n_genome, int32_t* Lc_out, int64_t* Lp_out, int32_t* F_prot_out,
+                  int32_t* F_genome_out, int32_t* T_out) {
+    if (!c) return PFAAI_ERR_INVALID;
+    if (n < 0 || n > kMaxF || n_prot < 1 || n_prot >= kMaxRuns || n_genome < 1)
+        return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: bad sizes (|F| <= 2^32 - 64, 1 <= n_prot < 4096)");
+    if ((n && (!prot || !genome || !tetra || !F_prot_out || !F_genome_out)) || !Lc_out || !Lp_out)
+        return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: null array");
+    {  // ranges, and every protein's triples in non-decreasing genome order (the stable sort keeps it)
+        std::vector<int32_t> last(n_prot, -1);
+        for (int64_t i = 0; i < n; ++i) {
+            const int32_t p = prot[i], g = genome[i], t = tetra[i];
+            if (p < 0 || p >= n_prot || g < 0 || g >= n_genome || t < 0 || t >= PFAAI_NTETRAMERS)
+                return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: protein, genome or tetramer id out of range");
+            if (g < last[p])
+                return fail(c, PFAAI_ERR_INVALID,
+                            "pfaai_build_f: triples of a protein must come in non-decreasing genome order");
+            last[p] = g;
+        }
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    const int64_t nn = std::max<int64_t>(n, 1);
+    const int64_t ntiles = ceil_div(nn, kRsTile), hist_n = kRsBins * ntiles;
+    DevBuf in_p, in_g, in_t, Tdev;
+    auto cleanup = [&]() { release(in_p); release(in_g); release(in_t); release(Tdev); };
+    if ((rc = upload(c, in_p, prot, n)) || (rc = upload(c, in_g, genome, n)) || (rc = upload(c, in_t, tetra, n))) {
+        cleanup();
+        return rc;
+    }
+    if ((rc = ensure(c, c->key_c, nn * 4)) || (rc = ensure(c, c->key_a, nn * 4)) || (rc = ensure(c, c->key_b, nn * 4)) ||
+        (rc = ensure(c, c->val_a, nn * 4)) || (rc = ensure(c, c->val_b, nn * 4)) || (rc = ensure(c, c->rec_c, nn * 8)) ||
+        (rc = ensure(c, c->recs, nn * 8)) || (rc = ensure(c, c->hist, hist_n * 4)) ||
+        (rc = ensure(c, c->hoff, (hist_n + 1) * 8)) || (rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * 4)) ||
+        (rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max<int64_t>(hist_n, PFAAI_NTETRAMERS), kScanTile)) * 8))) {
+        cleanup();
+        return rc;
+    }
+    const size_t tbytes = (size_t)n_prot * n_genome * sizeof(int32_t);
+    if (T_out && (rc = ensure(c, Tdev, tbytes))) { cleanup(); return rc; }
+    auto* cnt = static_cast<uint32_t*>(c->cnt_t.p);
+    HIPCHK(c, hipMemsetAsync(cnt, 0, PFAAI_NTETRAMERS * 4, s));
+    if (T_out) HIPCHK(c, hipMemsetAsync(Tdev.p, 0, tbytes, s));
+    auto* keys0 = static_cast<uint32_t*>(c->key_c.p);
+    auto* rec0 = static_cast<uint2*>(c->rec_c.p);
+    const int grid = (int)std::min<int64_t>(ceil_div(nn, 256), 8192);
+    if (n)
+        hipLaunchKernelGGL(k_f_keys, dim3(grid), dim3(256), 0, s, static_cast<const int32_t*>(in_p.p),
+                           static_cast<const int32_t*>(in_g.p), static_cast<const int32_t*>(in_t.p), n, n_prot,
+                           n_genome, keys0, rec0, cnt, static_cast<int32_t*>(T_out ? Tdev.p : nullptr));
+    HIPCHK(c, hipGetLastError());
+    auto* recs = static_cast<uint2*>(c->recs.p);
+    if (n) {
+        int bits = 1;
+        while (bits < 32 && ((int64_t)1 << bits) < (int64_t)PFAAI_NTETRAMERS * n_prot) ++bits;
+        const int passes = (bits + 7) / 8;
+        auto* hist = static_cast<uint32_t*>(c->hist.p);
+        auto* hoff = static_cast<unsigned long long*>(c->hoff.p);
+        uint32_t* kin = keys0;
+        uint32_t* vin = nullptr;
+        uint32_t* kout = static_cast<uint32_t*>(c->key_a.p);
+        uint32_t* vout = static_cast<uint32_t*>(c->val_a.p);
+        uint32_t* kalt = static_cast<uint32_t*>(c->key_b.p);
+        uint32_t* valt = static_cast<uint32_t*>(c->val_b.p);
+        for (int pass = 0; pass < passes; ++pass) {
+            const int shift = 8 * pass;
+            const bool first = pass == 0, last = pass == passes - 1;
+            hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kRsThreads), 0, s, kin, n, shift, hist, ntiles);
+            if ((rc = scan_u32(c, hist, hist_n, hoff, s))) { cleanup(); return rc; }
+#define RS(F, L)                                                                                                  \
+    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, hist, \
+                       ntiles, kout, vout, rec0, recs)
+            if (first && last) RS(true, true);
+            else if (first) RS(true, false);
+            else if (last) RS(false, true);
+            else RS(false, false);
+#undef RS
+            kin = kout;
+            vin = vout;
+            std::swap(kout, kalt);
+            std::swap(vout, valt);
+        }
+        // the F columns into two free key-sized buffers
+        int32_t* fp = reinterpret_cast<int32_t*>(kout);
+        int32_t* fg = reinterpret_cast<int32_t*>(vout);
+        hipLaunchKernelGGL(k_f_split, dim3(grid), dim3(256), 0, s, recs, n, fp, fg);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(F_prot_out, fp, n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(F_genome_out, fg, n * 4, hipMemcpyDeviceToHost, s));
+    }
+    std::vector<uint32_t> lc(PFAAI_NTETRAMERS);
+    HIPCHK(c, hipMemcpyAsync(lc.data(), cnt, PFAAI_NTETRAMERS * 4, hipMemcpyDeviceToHost, s));
+    if (T_out) HIPCHK(c, hipMemcpyAsync(T_out, Tdev.p, tbytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    cleanup();
+    c->wl_ready = false;  // the work-list buffers were resized / overwritten
+    Lp_out[0] = 0;
+    for (int t = 0; t < PFAAI_NTETRAMERS; ++t) {
+        Lc_out[t] = (int32_t)lc[t];
+        Lp_out[t + 1] = Lp_out[t] + lc[t];
+    }
+    return PFAAI_OK;
+}
+
 }  // extern "C"

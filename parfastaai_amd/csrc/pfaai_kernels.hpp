@@ -490,6 +490,39 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     }
 }
 
+// ---------------------------------------------------------------------------
+// K-F: F construction (pfaai_build_f).  The reference builds F with an SQL
+// UNION ALL + ORDER BY over the `<p>_tetras` tables (scp_db.hpp:161-216,
+// ds_helper.hpp:126-162) and Lc with per-protein range queries (82-122).
+// Here: (protein, genome, tetramer) triples -> key t * P + p, record (p, g);
+// the stable LSD radix sort above (k_rs_hist / k_rs_scatter) orders them by
+// (t, p) and, being stable, keeps each protein's ascending genome order, so
+// the sorted records are F by (tetramer, protein, genome).  Lc and T are
+// counted on the way in.
+// ---------------------------------------------------------------------------
+__global__ void k_f_keys(const int32_t* __restrict__ prot, const int32_t* __restrict__ genome,
+                         const int32_t* __restrict__ tetra, int64_t n, int32_t P, int32_t n_genome,
+                         uint32_t* __restrict__ keys, uint2* __restrict__ recs, uint32_t* __restrict__ lc,
+                         int32_t* __restrict__ T) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t p = prot[i], g = genome[i], t = tetra[i];
+        keys[i] = (uint32_t)t * (uint32_t)P + (uint32_t)p;
+        recs[i] = make_uint2((uint32_t)p, (uint32_t)g);
+        atomicAdd(&lc[t], 1u);
+        if (T) atomicAdd(&T[(int64_t)p * n_genome + g], 1);
+    }
+}
+
+// sorted (p, g) records -> the two F columns
+__global__ void k_f_split(const uint2* __restrict__ recs, int64_t n, int32_t* __restrict__ fp,
+                          int32_t* __restrict__ fg) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint2 r = recs[i];
+        fp[i] = (int32_t)r.x;
+        fg[i] = (int32_t)r.y;
+    }
+}
+
 // rowptr[k] = first sorted position with key >= k  (k in [0, K]).
 __global__ void k_rowptr(const uint32_t* __restrict__ keys, int64_t n, int64_t K,
                          unsigned long long* __restrict__ rowptr) {
