@@ -71,6 +71,21 @@ struct pfaai_ctx {
     // per-run event triples for pfaai_timing (pool reused after each reset)
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;
+    bool windows = false;  // this run: absolute column windows, a run table per window
+    // the next (start, after build, after rows) event triple of the pool
+    hipEvent_t* take_events() {
+        while (pool.size() < pool_used + 3) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        hipEvent_t* ev = &pool[pool_used];
+        pool_used += 3;
+        ev0 = ev[0];
+        ev1 = ev[1];
+        ev2 = ev[2];
+        return ev;
+    }
 };
 
 namespace {
@@ -213,7 +228,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
-    hipLaunchKernelGGL(k_blk, dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
+    hipLaunchKernelGGL(k_blk<false>, dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
                        (size_t)c->prob.n_prot * tile * sizeof(uint4), s, c->dev, tile,
                        getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0);
     if (first_event) {
@@ -247,6 +262,13 @@ int pick_kw(int32_t max_cols, int kw_max) {
     return kw_max;
 }
 
+// k_rows_pl's chunk width for this problem (launch_rows' KW choice)
+int64_t pl_chunk_cols(pfaai_ctx* c) {
+    if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->max_cols, 10);
+    const char* km = getenv("PFAAI_PL_KWMAX");
+    return 2 * 1024 * (int64_t)pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+}
+
 template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
@@ -256,12 +278,39 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
-    if (bigf)
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, true>), dim3(re - rb, nchunks), dim3(NT), lds, s,
-                           c->dev, rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else
-        hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(re - rb, nchunks), dim3(NT), lds, s, c->dev,
-                           rb, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    auto rows = [&](int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
+        if (bigf)
+            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, true>), dim3(r1 - r0, gy), dim3(NT), lds, s,
+                               c->dev, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+        else
+            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(r1 - r0, gy), dim3(NT), lds, s, c->dev,
+                               r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    };
+    if (nchunks == 1 || !c->windows) {
+        rows(rb, re, nchunks, -1);
+        return;
+    }
+    // rows wider than one chunk (c->windows, set by run_mode): per absolute
+    // column window, the run table of that window (k_blk<true>), then the
+    // rows that have columns in it; each window is its own event triple in
+    // the timing pool (pfaai_timing sums them)
+    const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
+    const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
+    const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
+    for (int32_t w = 0; w < nwin; ++w) {
+        int64_t r1 = re;
+        if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
+        if (r1 <= rb) continue;
+        hipEvent_t* ev = c->take_events();
+        if (!ev) return;
+        (void)hipEventRecord(ev[0], s);
+        hipLaunchKernelGGL((k_blk<true>), dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
+                           (size_t)c->prob.n_prot * tile * sizeof(uint4), s, c->dev, tile, 0, w * chunk,
+                           (w + 1) * chunk);
+        (void)hipEventRecord(ev[1], s);
+        rows(rb, r1, 1, w);
+        (void)hipEventRecord(ev[2], s);
+    }
 }
 
 
@@ -292,13 +341,13 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     if (c->rows_kernel == RK_PL) {
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
-        if (MODE == 0 && kw == 5 && getenv("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+        if (MODE == 0 && kw == 5 && !c->windows && getenv("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
             const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
             const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
             hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
-                               chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
+                               chunk, -1, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
                                static_cast<unsigned long long*>(c->dbg.p));
             return;
         }
@@ -377,19 +426,31 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     const bool compat = flags & PFAAI_FLAG_REF_COMPAT;
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     HIPCHK(c, hipMemsetAsync(sc + SC_EVENTS, 0, sizeof(unsigned long long), s));
-    // three events per run: start, after work-list build, after row kernel
-    while (c->pool.size() < c->pool_used + 3) {
-        hipEvent_t e;
-        HIPCHK(c, hipEventCreate(&e));
-        c->pool.push_back(e);
-    }
-    hipEvent_t* ev = &c->pool[c->pool_used];
-    c->pool_used += 3;
-    c->ev0 = ev[0];
-    c->ev1 = ev[1];
-    c->ev2 = ev[2];
-    HIPCHK(c, hipEventRecord(c->ev0, s));
     const bool wl = c->rows_kernel == RK_WORKLIST;
+    // rows wider than one k_rows_pl chunk: absolute column windows, each with
+    // its own run table (launch_pl); PFAAI_PL_WINDOWS=0 keeps the per-row
+    // chunks over one table (A/B)
+    {
+        const char* wv = getenv("PFAAI_PL_WINDOWS");
+        c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && !(wv && wv[0] == '0') &&
+                     (int64_t)c->max_cols + 1 > pl_chunk_cols(c);
+    }
+    if (c->windows) {
+        if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
+            int* err = reinterpret_cast<int*>(sc + SC_ERR);
+            HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+            hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
+                               (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
+                               static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
+        }
+        c->runs_valid = false;  // the table left behind is the last window's
+        launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
+        HIPCHK(c, hipGetLastError());
+        return PFAAI_OK;
+    }
+    // three events per run: start, after work-list build, after row kernel
+    if (!c->take_events()) return fail(c, PFAAI_ERR_HIP, "hipEventCreate failed");
+    HIPCHK(c, hipEventRecord(c->ev0, s));
     if (wl) {
         const int rcw = ensure_worklists(c);
         if (rcw) return rcw;

@@ -299,7 +299,14 @@ constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer f
 constexpr int kBlkLdsBytes = 64 << 10;  // its LDS staging: n_prot x tile x 16 B
 
 // dbg (diagnostics, PFAAI_BLK_ABLATE): bit 0 skips (1), bit 1 (2), bit 2 (3).
-__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg) {
+// WIN (column windows for rows wider than one row-kernel chunk): the table of
+// column window [wlo, whi) only -- each entry is the sub-run of members with
+// wlo <= genome < whi (contiguous: a run is sorted by genome), so a chunk of
+// the row kernel loads only the lines of its own window, and every chunk
+// launch works on the same 1/n_chunks of F (L2 / MALL locality).
+template <bool WIN = false>
+__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wlo = 0,
+                                                       int32_t whi = 0) {
     extern __shared__ uint4 ent[];  // [n_prot][kBlkTile] runs of the tile's tetramers
     __shared__ int64_t lp[kBlkTileMax + 1];
     const int tid = threadIdx.x, P = d.n_prot;
@@ -330,6 +337,19 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
         uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.x & 0xFFFFu), 0x130, 0xf, 0xf, false);  // wave_shl:1
         if (lane == 0) prev = c0 > S && in ? d.Fp16[c0 - 1] : 0xFFFFu;
         if (lane == 63) next = c0 + 8 < E ? d.Fp16[c0 + 8] : 0xFFFFu;
+        // WIN: the 8 genome ids too (Fg carries 16 padding entries), neighbours likewise
+        int32_t gg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int32_t gprev = 0, gnext = 0;
+        if constexpr (WIN) {
+            const uint4 ga = in ? *reinterpret_cast<const uint4*>(d.Fg + c0) : make_uint4(0u, 0u, 0u, 0u);
+            const uint4 gb = in ? *reinterpret_cast<const uint4*>(d.Fg + c0 + 4) : make_uint4(0u, 0u, 0u, 0u);
+            gg[0] = (int32_t)ga.x; gg[1] = (int32_t)ga.y; gg[2] = (int32_t)ga.z; gg[3] = (int32_t)ga.w;
+            gg[4] = (int32_t)gb.x; gg[5] = (int32_t)gb.y; gg[6] = (int32_t)gb.z; gg[7] = (int32_t)gb.w;
+            gprev = __builtin_amdgcn_update_dpp(0, (int)gb.w, 0x138, 0xf, 0xf, false);  // wave_shr:1
+            gnext = __builtin_amdgcn_update_dpp(0, (int)ga.x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+            if (lane == 0) gprev = c0 > S && in ? d.Fg[c0 - 1] : -1;
+            if (lane == 63) gnext = c0 + 8 < E ? d.Fg[c0 + 8] : 0x7FFFFFFF;
+        }
         if (!in) continue;
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
         int tl = tet_of(max(c0, S));
@@ -341,8 +361,15 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
             const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
             if (i < S || i >= E) continue;
             while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
-            if (i == lp[tl] || qp != q) ent[q * kBlkTile + tl].x = (uint32_t)i;
-            if (i + 1 == lp[tl + 1] || qn != q) ent[q * kBlkTile + tl].y = (uint32_t)(i + 1);
+            bool head = i == lp[tl] || qp != q, tail = i + 1 == lp[tl + 1] || qn != q;
+            if constexpr (WIN) {  // sub-run of the run inside [wlo, whi): ids ascend along a run
+                const int32_t g = gg[j], gp = j == 0 ? gprev : gg[j - 1], gn = j == 7 ? gnext : gg[j + 1];
+                if (g < wlo || g >= whi) continue;
+                head = head || gp < wlo;
+                tail = tail || gn >= whi;
+            }
+            if (head) ent[q * kBlkTile + tl].x = (uint32_t)i;
+            if (tail) ent[q * kBlkTile + tl].y = (uint32_t)(i + 1);
         }
     }
     __syncthreads();

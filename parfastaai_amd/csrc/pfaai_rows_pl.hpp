@@ -108,7 +108,8 @@ constexpr int kClkBlocks = 256;
 // NL: the per-column counts N live in LDS (u8 pairs, P <= 255) instead of
 // registers -- 5 VGPRs less at KW = 5, paid for with half the task capacity.
 template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false>
-__global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, uint32_t flags,
+__global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
+                                                   uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
                                                    double* __restrict__ aji, double* __restrict__ s_out,
                                                    int32_t* __restrict__ n_out,
@@ -130,8 +131,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
     row_cols<MODE>(d, a, clo, chi);
-    // chunks start at even columns so a counter word / T word holds columns (2w, 2w+1)
-    const int32_t cc0 = (clo & ~1) + (int32_t)blockIdx.y * chunk_cols;
+    // chunks start at even columns so a counter word / T word holds columns (2w, 2w+1);
+    // abs_chunk >= 0: one absolute column window [abs_chunk * chunk_cols, +chunk_cols),
+    // the one the run table was built for (k_blk<true>)
+    const int32_t cc0 = abs_chunk >= 0 ? abs_chunk * chunk_cols : (clo & ~1) + (int32_t)blockIdx.y * chunk_cols;
     const int32_t wlo = max(cc0, clo), whi = min(chi, cc0 + chunk_cols);
     if (wlo >= whi) return;  // uniform
     const int32_t ncw = (whi - cc0 + 1) >> 1;

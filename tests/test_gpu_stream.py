@@ -126,3 +126,32 @@ def test_f_beyond_2_30_entries(engine):
             k = n * a + b - (a + 2) * (a + 1) // 2 - f0
             assert np.array_equal(S[k], So[a - lo, b]) and np.array_equal(N[k], No[a - lo, b])
             assert np.array_equal(aji[k], np.where(N[k] > 0, S[k] / np.maximum(N[k], 1), 0.0))
+
+
+@pytest.mark.parametrize("mode", ["all", "qsub", "qt"])
+def test_column_windows_equal_row_chunks(engine, monkeypatch, mode):
+    """Rows wider than one k_rows_pl chunk: absolute column windows with a run
+    table per window (default) == per-row chunks over one table
+    (PFAAI_PL_WINDOWS=0, itself pinned against the oracle in
+    test_gpu_edges.py), S / N / AJI bit-exact, ref-compat included."""
+    if mode == "all":
+        pb = _all_problem(21000, 3, clade_size=50, n_random=1)
+    elif mode == "qsub":
+        g = syn.generate(11000, 4, clade_size=40, n_random=1)
+        pick = list(range(5, 11000, 197))
+        ds = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"],
+                                        [g["genome_set"][i] for i in pick])
+        pb = ds.with_genome_major(g["G_off"], g["G_tet"]).problem()
+    else:
+        pb = qt_syn(dict(n_tgt=12000, n_qry=40, n_prot=4, clade_size=30, n_random=1), genome_major=True).problem()
+    engine.load(**pb)
+    for flags in (0, _capi.FLAG_REF_COMPAT):
+        monkeypatch.delenv("PFAAI_PL_WINDOWS", raising=False)
+        a1, S1, N1 = engine.compute(flags)
+        ne1 = engine.stats()["n_events"]
+        monkeypatch.setenv("PFAAI_PL_WINDOWS", "0")
+        a2, S2, N2 = engine.compute(flags)
+        ne2 = engine.stats()["n_events"]
+        assert ne1 == ne2
+        assert np.array_equal(N1, N2) and np.array_equal(S1, S2) and np.array_equal(a1, a2)
+    monkeypatch.delenv("PFAAI_PL_WINDOWS", raising=False)
