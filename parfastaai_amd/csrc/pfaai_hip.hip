@@ -72,6 +72,9 @@ struct pfaai_ctx {
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;
     bool windows = false;  // this run: absolute column windows, a run table per window
+    DevBuf blkw;           // the window tables (window-major), built by k_blk<true>
+    bool win_valid = false, win_key = false;
+    int64_t win_cols = 0;
     // the next (start, after build, after rows) event triple of the pool
     hipEvent_t* take_events() {
         while (pool.size() < pool_used + 3) {
@@ -278,41 +281,32 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
-    auto rows = [&](int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
+    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
         if (bigf)
             hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, true>), dim3(r1 - r0, gy), dim3(NT), lds, s,
-                               c->dev, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+                               dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
         else
-            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(r1 - r0, gy), dim3(NT), lds, s, c->dev,
+            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv,
                                r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
     };
     if (nchunks == 1 || !c->windows) {
-        rows(rb, re, nchunks, -1);
+        rows(c->dev, rb, re, nchunks, -1);
         return;
     }
-    // rows wider than one chunk (c->windows, set by run_mode): per absolute
-    // column window, the run table of that window (k_blk<true>), then the
-    // rows that have columns in it; each window is its own event triple in
-    // the timing pool (pfaai_timing sums them)
+    // rows wider than one chunk (c->windows, set by run_mode, which built the
+    // window tables): per absolute column window, the rows with columns in it
+    // over that window's table
     const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
     const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
-    const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
     for (int32_t w = 0; w < nwin; ++w) {
         int64_t r1 = re;
         if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
         if (r1 <= rb) continue;
-        hipEvent_t* ev = c->take_events();
-        if (!ev) return;
-        (void)hipEventRecord(ev[0], s);
-        hipLaunchKernelGGL((k_blk<true>), dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
-                           (size_t)c->prob.n_prot * tile * sizeof(uint4), s, c->dev, tile, 0, w * chunk,
-                           (w + 1) * chunk);
-        (void)hipEventRecord(ev[1], s);
-        rows(rb, r1, 1, w);
-        (void)hipEventRecord(ev[2], s);
+        Dev dw = c->dev;
+        dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
+        rows(dw, rb, r1, 1, w);
     }
 }
-
 
 template <int MODE, int KW>
 void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
@@ -430,22 +424,48 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     // rows wider than one k_rows_pl chunk: absolute column windows, each with
     // its own run table (launch_pl); PFAAI_PL_WINDOWS=0 keeps the per-row
     // chunks over one table (A/B)
+    int win_tile = 0, nwin = 1;
+    const int64_t wcols = pl_chunk_cols(c);
     {
         const char* wv = getenv("PFAAI_PL_WINDOWS");
         c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && !(wv && wv[0] == '0') &&
-                     (int64_t)c->max_cols + 1 > pl_chunk_cols(c);
+                     (int64_t)c->max_cols + 1 > wcols;
+        if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 64 KB of LDS
+            nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
+            win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * (int64_t)c->prob.n_prot * nwin));
+            c->windows = win_tile >= 1 &&
+                         ensure(c, c->blkw, (size_t)nwin * c->prob.n_prot * kNTetramers * sizeof(uint4)) == PFAAI_OK;
+        }
     }
     if (c->windows) {
-        if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
-            int* err = reinterpret_cast<int*>(sc + SC_ERR);
-            HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
-            hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
-                               (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
-                               static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
+        if (!c->take_events()) return fail(c, PFAAI_ERR_HIP, "hipEventCreate failed");
+        HIPCHK(c, hipEventRecord(c->ev0, s));
+        // the window tables depend only on the loaded F and the window width
+        const bool keep = (flags & PFAAI_FLAG_KEEP_RUNS) && c->win_valid && c->win_cols == wcols &&
+                          (c->win_key || !compat);
+        if (!keep) {
+            Dev dw = c->dev;
+            dw.blk = static_cast<uint4*>(c->blkw.p);
+            hipLaunchKernelGGL((k_blk<true>), dim3(ceil_div(kNTetramers, win_tile)), dim3(kTetraThreads),
+                               (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4), s, dw, win_tile, 0,
+                               (int32_t)wcols, nwin);
+            if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
+                int* err = reinterpret_cast<int*>(sc + SC_ERR);
+                HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+                hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
+                                   (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr),
+                                   static_cast<uint2*>(nullptr), static_cast<const unsigned long long*>(nullptr),
+                                   sc + SC_FIRST_KEY, err);
+            }
+            HIPCHK(c, hipGetLastError());
+            c->win_valid = true;
+            c->win_key = compat;
+            c->win_cols = wcols;
         }
-        c->runs_valid = false;  // the table left behind is the last window's
+        HIPCHK(c, hipEventRecord(c->ev1, s));
         launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
         HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev2, s));
         return PFAAI_OK;
     }
     // three events per run: start, after work-list build, after row kernel
@@ -510,7 +530,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
-                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg})
+                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw})
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     release(c->st_dev);
@@ -556,6 +576,7 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
 
     c->prob = p;
     c->runs_valid = c->runs_key = false;
+    c->win_valid = c->win_key = false;
     const int32_t ni = p.n_ids;
     // output rows and derived maps
     std::vector<int32_t> row_of(ni, -1), tcol_row(ni), tcol_col(ni);

@@ -299,21 +299,32 @@ constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer f
 constexpr int kBlkLdsBytes = 64 << 10;  // its LDS staging: n_prot x tile x 16 B
 
 // dbg (diagnostics, PFAAI_BLK_ABLATE): bit 0 skips (1), bit 1 (2), bit 2 (3).
-// WIN (column windows for rows wider than one row-kernel chunk): the table of
-// column window [wlo, whi) only -- each entry is the sub-run of members with
-// wlo <= genome < whi (contiguous: a run is sorted by genome), so a chunk of
-// the row kernel loads only the lines of its own window, and every chunk
-// launch works on the same 1/n_chunks of F (L2 / MALL locality).
+// WIN (column windows for rows wider than one row-kernel chunk): one table
+// per absolute column window w = [w * wcols, (w + 1) * wcols), all built in
+// this one pass over F, window-major at blk + w * P * 160000 -- each entry is
+// the sub-run of the run's members in window w (contiguous: a run is sorted
+// by genome), so a row-kernel launch over window w loads only the lines of
+// that window, and all its workgroups work on the same 1/nwin of F (L2 / MALL
+// locality).  The LDS staging then holds nwin tables (fewer tetramers per tile).
+__device__ __forceinline__ int32_t win_of(int32_t g, int32_t wcols, float inv) {
+    int32_t w = (int32_t)((float)g * inv);  // g < 2^21: off by at most one, fixed below
+    if (w * wcols > g) --w;
+    if ((w + 1) * wcols <= g) ++w;
+    return w;
+}
+
 template <bool WIN = false>
-__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wlo = 0,
-                                                       int32_t whi = 0) {
-    extern __shared__ uint4 ent[];  // [n_prot][kBlkTile] runs of the tile's tetramers
+__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wcols = 0,
+                                                       int32_t nwin = 1) {
+    extern __shared__ uint4 ent[];  // [nwin][n_prot][kBlkTile] runs of the tile's tetramers
     __shared__ int64_t lp[kBlkTileMax + 1];
     const int tid = threadIdx.x, P = d.n_prot;
     const int t0 = blockIdx.x * kBlkTile;
     const int nt = min(kBlkTile, kNTetramers - t0);
+    const float inv = WIN ? 1.0f / (float)wcols : 0.0f;
+    const int PW = P * kBlkTile;  // entries per window
     // splitter fields start all-ones (kSplitNone); present ones are ANDed in
-    for (int k = tid; k < P * kBlkTile; k += kTetraThreads) ent[k] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0x7FFFFFFFu);
+    for (int k = tid; k < (WIN ? nwin : 1) * PW; k += kTetraThreads) ent[k] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0x7FFFFFFFu);
     if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
     __syncthreads();
     const int64_t S = lp[0], E = lp[nt];
@@ -362,14 +373,16 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
             if (i < S || i >= E) continue;
             while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
             bool head = i == lp[tl] || qp != q, tail = i + 1 == lp[tl + 1] || qn != q;
-            if constexpr (WIN) {  // sub-run of the run inside [wlo, whi): ids ascend along a run
+            int wo = 0;  // window table offset
+            if constexpr (WIN) {  // sub-runs by window: ids ascend along a run
                 const int32_t g = gg[j], gp = j == 0 ? gprev : gg[j - 1], gn = j == 7 ? gnext : gg[j + 1];
-                if (g < wlo || g >= whi) continue;
-                head = head || gp < wlo;
-                tail = tail || gn >= whi;
+                const int32_t w = win_of(g, wcols, inv);
+                head = head || gp < w * wcols;
+                tail = tail || gn >= (w + 1) * wcols;
+                wo = w * PW;
             }
-            if (head) ent[q * kBlkTile + tl].x = (uint32_t)i;
-            if (tail) ent[q * kBlkTile + tl].y = (uint32_t)(i + 1);
+            if (head) ent[wo + q * kBlkTile + tl].x = (uint32_t)i;
+            if (tail) ent[wo + q * kBlkTile + tl].y = (uint32_t)(i + 1);
         }
     }
     __syncthreads();
@@ -391,7 +404,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + (int64_t)u * kTetraThreads * kGroup;
             if (i >= E) continue;
-            uint4* r = &ent[q[u] * kBlkTile + tet_of(i)];
+            uint4* r = &ent[(WIN ? win_of((int32_t)g[u], wcols, inv) * PW : 0) + q[u] * kBlkTile + tet_of(i)];
             const uint32_t k = (uint32_t)(i - (r->x & ~(uint32_t)(kGroup - 1))) / kGroup;  // line of the run
             if (k < 1 || k > (uint32_t)kSplitters) continue;
             const uint64_t field = ~(kSplitNone << (kSplitBits * (k - 1))) | ((uint64_t)g[u] << (kSplitBits * (k - 1)));
@@ -400,8 +413,8 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
         }
     }
     __syncthreads();
-    // (3) write out: 16 consecutive entries of one protein per 256 B
-    for (int k = tid; k < P * kBlkTile && !(dbg & 4); k += kTetraThreads) {
+    // (3) write out: consecutive entries of one protein (and window) per tile
+    for (int k = tid; k < (WIN ? nwin : 1) * PW && !(dbg & 4); k += kTetraThreads) {
         const int tl = k % kBlkTile;
         if (tl < nt) d.blk[(int64_t)(k / kBlkTile) * kNTetramers + t0 + tl] = ent[k];
     }

@@ -139,6 +139,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     if (wlo >= whi) return;  // uniform
     const int32_t ncw = (whi - cc0 + 1) >> 1;
     const bool compat = flags & 1u;
+    const uint32_t min_len = abs_chunk >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int j = 0; j < EPT; ++j) {
             const int e = tid + j * NT;
             uint2 r;
-            nl[j] = run_lines(r4[j], wlo, whi, r);
+            nl[j] = run_lines(r4[j], wlo, whi, r, min_len);
             rt[st][e] = r;
             if (nl[j] > (uint32_t)kPlMaxLines) {
                 atomicOr(&wmask[cs][e >> 5], 1u << (e & 31));

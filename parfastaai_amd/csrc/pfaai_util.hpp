@@ -38,9 +38,12 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 
 // Run-table entry -> member range [lo, hi) and its line count after pruning
 // to the column window [wlo, whi) with the run's line splitters (k_blk).
-__device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi, uint2& r) {
+// min_len: a full run of one member is A alone (no partner), so runs of
+// length <= 1 are skipped; a column-window sub-run (k_blk<true>) may omit A,
+// and one member is then a partner (min_len 0).
+__device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi, uint2& r, uint32_t min_len = 1u) {
     r = make_uint2(r4.x, r4.y);
-    if (r.y - r.x <= 1u) return 0u;  // a run of one member is A alone: no partner
+    if (r.y - r.x <= min_len) return 0u;
     const uint32_t first = r.x & ~(uint32_t)(kGroup - 1);
     uint32_t nl = (r.y - first + kGroup - 1) / kGroup;
     if (nl > 1u) {

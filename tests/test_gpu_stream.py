@@ -154,4 +154,10 @@ def test_column_windows_equal_row_chunks(engine, monkeypatch, mode):
         ne2 = engine.stats()["n_events"]
         assert ne1 == ne2
         assert np.array_equal(N1, N2) and np.array_equal(S1, S2) and np.array_equal(a1, a2)
-    monkeypatch.delenv("PFAAI_PL_WINDOWS", raising=False)
+        monkeypatch.delenv("PFAAI_PL_WINDOWS", raising=False)
+        if mode != "qsub":  # streamed row tiles reuse the window tables (PFAAI_FLAG_KEEP_RUNS)
+            rows = engine.shape()[0]
+            a3, S3, N3, ne3, nt = _collect(engine, 0, rows, 3_000_000 if mode == "all" else 100_000,
+                                           flags | _capi.FLAG_EMIT_JAC)
+            assert nt > 1 and ne3 == ne1
+            assert np.array_equal(a3, a1) and np.array_equal(S3, S1) and np.array_equal(N3, N1)
