@@ -231,9 +231,15 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
-    hipLaunchKernelGGL(k_blk<false>, dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads),
-                       (size_t)c->prob.n_prot * tile * sizeof(uint4), s, c->dev, tile,
-                       getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0);
+    const int dbg = getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0;
+    const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
+    const char* bt = getenv("PFAAI_BLK_THREADS");  // A/B: 256 (default) | 1024
+    if (bt && atoi(bt) == 1024)
+        hipLaunchKernelGGL((k_blk<false, 1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile,
+                           dbg, 0, 1);
+    else
+        hipLaunchKernelGGL((k_blk<false, kTetraThreads>), dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads), lds, s,
+                           c->dev, tile, dbg, 0, 1);
     if (first_event) {
         HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
         hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
@@ -446,9 +452,16 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         if (!keep) {
             Dev dw = c->dev;
             dw.blk = static_cast<uint4*>(c->blkw.p);
-            hipLaunchKernelGGL((k_blk<true>), dim3(ceil_div(kNTetramers, win_tile)), dim3(kTetraThreads),
-                               (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4), s, dw, win_tile, 0,
-                               (int32_t)wcols, nwin);
+            // 1024 threads: the 64 KB of LDS staging allows two workgroups per
+            // CU, so a 256-thread form ran 8 waves per CU (PFAAI_BLK_THREADS=256 A/B)
+            const size_t lds = (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4);
+            const char* bt = getenv("PFAAI_BLK_THREADS");
+            if (bt && atoi(bt) == 256)
+                hipLaunchKernelGGL((k_blk<true, 256>), dim3(ceil_div(kNTetramers, win_tile)), dim3(256), lds, s, dw,
+                                   win_tile, 0, (int32_t)wcols, nwin);
+            else
+                hipLaunchKernelGGL((k_blk<true, 1024>), dim3(ceil_div(kNTetramers, win_tile)), dim3(1024), lds, s, dw,
+                                   win_tile, 0, (int32_t)wcols, nwin);
             if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
                 int* err = reinterpret_cast<int*>(sc + SC_ERR);
                 HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));

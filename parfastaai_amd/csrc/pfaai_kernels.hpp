@@ -313,8 +313,8 @@ __device__ __forceinline__ int32_t win_of(int32_t g, int32_t wcols, float inv) {
     return w;
 }
 
-template <bool WIN = false>
-__global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wcols = 0,
+template <bool WIN = false, int NTH = kTetraThreads>
+__global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wcols = 0,
                                                        int32_t nwin = 1) {
     extern __shared__ uint4 ent[];  // [nwin][n_prot][kBlkTile] runs of the tile's tetramers
     __shared__ int64_t lp[kBlkTileMax + 1];
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
     const float inv = WIN ? 1.0f / (float)wcols : 0.0f;
     const int PW = P * kBlkTile;  // entries per window
     // splitter fields start all-ones (kSplitNone); present ones are ANDed in
-    for (int k = tid; k < (WIN ? nwin : 1) * PW; k += kTetraThreads) ent[k] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0x7FFFFFFFu);
+    for (int k = tid; k < (WIN ? nwin : 1) * PW; k += NTH) ent[k] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0x7FFFFFFFu);
     if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
     __syncthreads();
     const int64_t S = lp[0], E = lp[nt];
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
     // shifts) or, at wave edges, from one extra load.
     const int lane = tid & 63;
     for (int64_t c0 = (S & ~(int64_t)7) + (int64_t)tid * 8; c0 - (int64_t)lane * 8 < E && !(dbg & 1);
-         c0 += (int64_t)kTetraThreads * 8) {  // wave-uniform trip count (DPP needs the whole wave)
+         c0 += (int64_t)NTH * 8) {  // wave-uniform trip count (DPP needs the whole wave)
         const bool in = c0 < E;
         const uint4 v = in ? *reinterpret_cast<const uint4*>(d.Fp16 + c0) : make_uint4(0u, 0u, 0u, 0u);
         uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.w >> 16), 0x138, 0xf, 0xf, false);  // wave_shr:1
@@ -392,17 +392,17 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
     // share of Fg is streamed once, one id per 64-B line, instead of being
     // gathered run by run.
     for (int64_t i0 = ((S + kGroup - 1) & ~(int64_t)(kGroup - 1)) + (int64_t)tid * kGroup; i0 < E && !(dbg & 2);
-         i0 += (int64_t)U * kTetraThreads * kGroup) {
+         i0 += (int64_t)U * NTH * kGroup) {
         uint32_t g[U], q[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + (int64_t)u * kTetraThreads * kGroup;
+            const int64_t i = i0 + (int64_t)u * NTH * kGroup;
             g[u] = i < E ? (uint32_t)d.Fg[i] : 0u;
             q[u] = i < E ? d.Fp16[i] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + (int64_t)u * kTetraThreads * kGroup;
+            const int64_t i = i0 + (int64_t)u * NTH * kGroup;
             if (i >= E) continue;
             uint4* r = &ent[(WIN ? win_of((int32_t)g[u], wcols, inv) * PW : 0) + q[u] * kBlkTile + tet_of(i)];
             const uint32_t k = (uint32_t)(i - (r->x & ~(uint32_t)(kGroup - 1))) / kGroup;  // line of the run
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_blk(Dev d, int kBlkTile, int 
     }
     __syncthreads();
     // (3) write out: consecutive entries of one protein (and window) per tile
-    for (int k = tid; k < (WIN ? nwin : 1) * PW && !(dbg & 4); k += kTetraThreads) {
+    for (int k = tid; k < (WIN ? nwin : 1) * PW && !(dbg & 4); k += NTH) {
         const int tl = k % kBlkTile;
         if (tl < nt) d.blk[(int64_t)(k / kBlkTile) * kNTetramers + t0 + tl] = ent[k];
     }
