@@ -233,13 +233,15 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
     const int dbg = getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0;
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
-    const char* bt = getenv("PFAAI_BLK_THREADS");  // A/B: 256 (default) | 1024
-    if (bt && atoi(bt) == 1024)
-        hipLaunchKernelGGL((k_blk<false, 1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile,
-                           dbg, 0, 1);
-    else
+    // 1024 threads (0.649 vs 0.666 ms at 10k; the window form gains 2x, see
+    // run_mode); PFAAI_BLK_THREADS=256 for A/B
+    const char* bt = getenv("PFAAI_BLK_THREADS");
+    if (bt && atoi(bt) == 256)
         hipLaunchKernelGGL((k_blk<false, kTetraThreads>), dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads), lds, s,
                            c->dev, tile, dbg, 0, 1);
+    else
+        hipLaunchKernelGGL((k_blk<false, 1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile,
+                           dbg, 0, 1);
     if (first_event) {
         HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
         hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
@@ -453,7 +455,8 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
             Dev dw = c->dev;
             dw.blk = static_cast<uint4*>(c->blkw.p);
             // 1024 threads: the 64 KB of LDS staging allows two workgroups per
-            // CU, so a 256-thread form ran 8 waves per CU (PFAAI_BLK_THREADS=256 A/B)
+            // CU, so a 256-thread form ran 8 waves per CU (PFAAI_BLK_THREADS=256
+            // A/B: 6.0 -> 2.9 ms at QT 50 000 x 1 000)
             const size_t lds = (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4);
             const char* bt = getenv("PFAAI_BLK_THREADS");
             if (bt && atoi(bt) == 256)
