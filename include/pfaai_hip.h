@@ -168,6 +168,15 @@ int pfaai_stream(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, int64_t til
 /* |E| summed over the tiles of the last pfaai_stream. */
 int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 
+/* Rows [row_begin, row_end) into HOST arrays of length n_pairs indexed by
+ * the JAC index (only the rows' entries are written; any may be NULL).
+ * Synchronous.  ALL and QT: disjoint row blocks have disjoint spans, so one
+ * host thread per context (one context per device) fills a shared host
+ * array for a multi-GPU run without a gather (CLI --devices; the C++
+ * adapter's multi-device constructor).  QSUB: all rows only. */
+int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
+                       double* h_aji, double* h_S, int32_t* h_N);
+
 /* |E| of the last run, counted by the scatter kernel (equals the reference's
  * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and
  * device times (ms) of its two phases: work-list build, row kernel.

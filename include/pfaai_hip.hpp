@@ -15,8 +15,10 @@
 // classes of parfastaai_amd/host/datastruct.hpp.  The mode is deduced from the
 // DSIT (pfaai_mode_of<DSIT>) or passed explicitly.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -42,7 +44,27 @@ class ParFAAIHipImpl {
         if (rc) throw HipError(rc, "pfaai_create failed (no visible MI355X?)");
         upload();
     }
-    ~ParFAAIHipImpl() { pfaai_destroy(m_ctx); }
+    // Multi-GPU (one process, one context per device, one host thread per
+    // context): rows are split by the row-cost model of parfastaai_amd/shard.py
+    // and every device writes its rows' JAC span of the shared host arrays
+    // (pfaai_compute_rows); ALL and QT -- QSUB runs on devices[0].
+    ParFAAIHipImpl(const DSIT& ds, int mode, const std::vector<int>& devices, bool ref_compat = false)
+        : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
+        if (devices.empty()) throw HipError(PFAAI_ERR_INVALID, "no device");
+        int rc = pfaai_create(&m_ctx, devices[0]);
+        if (rc) throw HipError(rc, "pfaai_create failed (no visible MI355X?)");
+        for (std::size_t i = 1; i < devices.size() && mode != PFAAI_MODE_QSUB; ++i) {
+            pfaai_ctx* x = nullptr;
+            rc = pfaai_create(&x, devices[i]);
+            if (rc) throw HipError(rc, "pfaai_create failed for device " + std::to_string(devices[i]));
+            m_extra.push_back(x);
+        }
+        upload();
+    }
+    ~ParFAAIHipImpl() {
+        pfaai_destroy(m_ctx);
+        for (pfaai_ctx* x : m_extra) pfaai_destroy(x);
+    }
     ParFAAIHipImpl(const ParFAAIHipImpl&) = delete;
     ParFAAIHipImpl& operator=(const ParFAAIHipImpl&) = delete;
 
@@ -61,13 +83,18 @@ class ParFAAIHipImpl {
         std::vector<double> S(n);
         std::vector<int32_t> N(n);
         m_AJIdev.resize(n);
-        int rc = pfaai_compute(m_ctx, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, m_AJIdev.data(), S.data(), N.data());
-        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
+        if (m_extra.empty()) {
+            int rc = pfaai_compute(m_ctx, flags, m_AJIdev.data(), S.data(), N.data());
+            if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        } else {
+            computeMulti(flags, S.data(), N.data());
+        }
         for (std::size_t i = 0; i < n; ++i) {
             m_JAC[i].S = S[i];
             m_JAC[i].N = N[i];
         }
-        pfaai_last_stats(m_ctx, &m_events, &m_msBuild, &m_msRows);
+        if (m_extra.empty()) pfaai_last_stats(m_ctx, &m_events, &m_msBuild, &m_msRows);
         return 0;  // PFAAI_OK
     }
     // algorithm_impl.hpp:309-322 (the kernel epilogue already divided S / N)
@@ -113,7 +140,56 @@ class ParFAAIHipImpl {
     float msBuild() const { return m_msBuild; }
     float msRows() const { return m_msRows; }
 
+    int nDevices() const { return 1 + (int)m_extra.size(); }
+
   private:
+    // contiguous row blocks balanced by the row-cost model (shard.py:split_rows)
+    static std::vector<int64_t> splitRows(int64_t n, int parts, bool all_vs_all) {
+        std::vector<int64_t> cut{0};
+        const double k = 0.75 * (double)n;  // shard.FIXED_COST_FRACTION
+        auto before = [&](int64_t a) {
+            return all_vs_all ? (double)a * k + (double)a * n - (double)a * (a + 1) / 2.0 : (double)a;
+        };
+        const double total = before(n);
+        for (int r = 1; r < parts; ++r) {
+            int64_t lo = cut.back(), hi = n;
+            const double target = total * r / parts;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) / 2;
+                if (before(mid) < target) lo = mid + 1; else hi = mid;
+            }
+            cut.push_back(lo);
+        }
+        cut.push_back(n);
+        return cut;
+    }
+    void computeMulti(uint32_t flags, double* S, int32_t* N) {
+        int64_t rows = 0, pairs = 0;
+        pfaai_shape(m_ctx, &rows, &pairs);
+        std::vector<pfaai_ctx*> ctx{m_ctx};
+        ctx.insert(ctx.end(), m_extra.begin(), m_extra.end());
+        const auto cut = splitRows(rows, (int)ctx.size(), m_mode == PFAAI_MODE_ALL);
+        std::vector<int> rcs(ctx.size(), 0);
+        std::vector<std::thread> th;
+        for (std::size_t i = 0; i < ctx.size(); ++i)
+            th.emplace_back([&, i] {
+                rcs[i] = pfaai_compute_rows(ctx[i], cut[i], cut[i + 1], flags, m_AJIdev.data(), S, N);
+            });
+        for (auto& t : th) t.join();
+        m_events = 0;
+        m_msBuild = m_msRows = 0.f;
+        for (std::size_t i = 0; i < ctx.size(); ++i) {
+            if (rcs[i]) throw HipError(rcs[i], pfaai_last_error(ctx[i]));
+            if (cut[i + 1] == cut[i]) continue;
+            int64_t e = 0;
+            float b = 0.f, r = 0.f;
+            pfaai_last_stats(ctx[i], &e, &b, &r);
+            m_events += e;
+            m_msBuild = std::max(m_msBuild, b);
+            m_msRows = std::max(m_msRows, r);
+        }
+    }
+
     void upload() {
         const auto& Lp32 = m_ds.refLp();
         const auto& Lc = m_ds.refLc();
@@ -169,12 +245,15 @@ class ParFAAIHipImpl {
         }
         int rc = pfaai_load(m_ctx, &pb);
         if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        for (pfaai_ctx* x : m_extra)
+            if ((rc = pfaai_load(x, &pb))) throw HipError(rc, pfaai_last_error(x));
     }
 
     const DSIT& m_ds;
     int m_mode;
     bool m_compat;
     pfaai_ctx* m_ctx = nullptr;
+    std::vector<pfaai_ctx*> m_extra;  // further devices (multi-GPU constructor)
     std::vector<int64_t> m_Lp;
     std::vector<int32_t> m_Fp, m_Fg, m_T, m_qidx, m_trank;
     std::vector<uint8_t> m_isq;

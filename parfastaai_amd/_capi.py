@@ -33,7 +33,7 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f",
+    "pfaai_build_f", "pfaai_compute_rows",
 ]
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
@@ -91,6 +91,7 @@ def load_library():
         "pfaai_device_free": (ctypes.c_int, [vp, vp]),
         "pfaai_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, i64]),
         "pfaai_synchronize": (ctypes.c_int, [vp]),
+        "pfaai_compute_rows": (ctypes.c_int, [vp, i64, i64, u32, vp, vp, vp]),
         "pfaai_build_f": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),

@@ -1253,4 +1253,40 @@ int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, cons
     return PFAAI_OK;
 }
 
+
+// Rows into host arrays at their JAC span: one thread per context (device)
+// runs its own row block; the spans of disjoint row blocks are disjoint in
+// ALL and QT, so several devices fill one host JAC array without a gather.
+int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* h_aji, double* h_S,
+                       int32_t* h_N) {
+    if (!c) return PFAAI_ERR_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
+    if (c->prob.mode == PFAAI_MODE_QSUB && !(rb == 0 && re == c->n_rows))
+        return fail(c, PFAAI_ERR_INVALID, "pfaai_compute_rows: QSUB row blocks have no contiguous JAC span");
+    if (rb == re) return PFAAI_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int64_t f = 0, n = 0;
+    pfaai_row_span(c, rb, re, &f, &n);
+    int rc;
+    if ((rc = ensure(c, c->out_aji, n * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_S, n * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_N, n * sizeof(int32_t)))) return rc;
+    auto* aji = static_cast<double*>(c->out_aji.p);
+    auto* S = static_cast<double*>(c->out_S.p);
+    auto* N = static_cast<int32_t*>(c->out_N.p);
+    if (c->prob.mode == PFAAI_MODE_QSUB) {  // the hull holds every pair; the kernel writes them all
+        HIPCHK(c, hipMemsetAsync(aji, 0, n * sizeof(double), c->stream));
+        HIPCHK(c, hipMemsetAsync(S, 0, n * sizeof(double), c->stream));
+        HIPCHK(c, hipMemsetAsync(N, 0, n * sizeof(int32_t), c->stream));
+    }
+    rc = pfaai_run(c, rb, re, flags | PFAAI_FLAG_EMIT_JAC, aji - f, S - f, N - f, c->stream);
+    if (rc) return rc;
+    if (h_aji) HIPCHK(c, hipMemcpyAsync(h_aji + f, aji, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (h_S) HIPCHK(c, hipMemcpyAsync(h_S + f, S, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (h_N) HIPCHK(c, hipMemcpyAsync(h_N + f, N, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_OK;
+}
+
 }  // extern "C"

@@ -23,6 +23,8 @@
 #include <vector>
 
 #include "datastruct.hpp"
+#include <sstream>
+
 #include "output.hpp"
 #include "pfaai_hip.hpp"
 #include "scp_db.hpp"
@@ -42,6 +44,7 @@ struct AppParams {  // main.cpp:56-131
     std::string formatSelftest;  // --format-selftest FILE: print fmt-formatted doubles (hex input)
     std::string streamAji;       // --stream-aji FILE: pfaai_stream the AJI vector to FILE (no CSV)
     long long tilePairs = 1ll << 27;
+    std::vector<int> devices;    // --devices 0,1,...: one context per device, rows split (ALL / QT)
 
     void print() const {
         std::vector<std::string> args = {" Input Database  : " + pathToDatabase + " ",
@@ -83,6 +86,7 @@ const char* kUsage =
     "  -q,--query_subset TEXT:FILE  Path to Query List (Should be subset of genomoes in the input DB.)\n"
     "  --ref-compat             Reproduce the reference's quirks (zero-overlap pairs, QT T indexing)\n"
     "  --device INT [0]         HIP device\n"
+    "  --devices LIST           Comma-separated HIP devices: rows split over them (all-vs-all, -r)\n"
     "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n"
     "  --stream-aji TEXT        Stream the AJI vector (JAC-index order, cereal vector<double>) to FILE\n"
     "                           tile by tile instead of writing the CSV matrix (-q not supported)\n"
@@ -123,6 +127,14 @@ int parse(int argc, char** argv, AppParams& a) {
             a.device = std::atoi(v.c_str());
         } else if (is("--stream-aji", "--stream-aji")) {
             if (!value(a.streamAji)) return 114;
+        } else if (is("--devices", "--devices")) {
+            std::string v;
+            if (!value(v)) return 114;
+            std::stringstream ss(v);
+            std::string tok;
+            while (std::getline(ss, tok, ','))
+                if (!tok.empty()) a.devices.push_back(std::atoi(tok.c_str()));
+            if (a.devices.empty()) return 105;
         } else if (is("--tile-pairs", "--tile-pairs")) {
             std::string v;
             if (!value(v)) return 114;
@@ -202,7 +214,8 @@ template <typename DS>
 int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
     auto t0 = std::chrono::steady_clock::now();
     try {
-        pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, app.device, app.refCompat);
+        const std::vector<int> devs = app.devices.empty() ? std::vector<int>{app.device} : app.devices;
+        pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, devs, app.refCompat);
         if (!app.streamAji.empty()) {  // output-tile streaming: no CSV, no whole matrix anywhere
             if (mode == PFAAI_MODE_QSUB) {
                 std::cerr << "--stream-aji does not support -q" << std::endl;
@@ -214,8 +227,8 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
             return rc;
         }
         impl.run();
-        std::printf("AJI (MI355X)        : %10.2f ms  (|E| = %lld; work lists %.2f ms, rows %.2f ms)\n",
-                    ms_since(t0), (long long)impl.nEvents(), impl.msBuild(), impl.msRows());
+        std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; run tables %.2f ms, rows %.2f ms)\n",
+                    impl.nDevices(), ms_since(t0), (long long)impl.nEvents(), impl.msBuild(), impl.msRows());
         if (app.pathToOutputFile.empty()) return 0;
         auto t1 = std::chrono::steady_clock::now();
         std::printf("Writing output with %lld query genomes and %lld target genomes. \n",

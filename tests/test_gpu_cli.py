@@ -31,11 +31,12 @@ def run(*args):
     return r
 
 
+@pytest.mark.parametrize("devs", [[], ["--devices", "0,0"]], ids=["1dev", "2ctx"])
 @pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
-def test_cli_csv_bytes(tmp_path, name):
+def test_cli_csv_bytes(tmp_path, name, devs):
     db = unpack(tmp_path, name + ".db")
     out = tmp_path / "out.csv"
-    run(db, str(out), "--bin", str(tmp_path / "o"))
+    run(db, str(out), "--bin", str(tmp_path / "o"), *devs)
     assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
     J = fm.read_jac(str(tmp_path / "o_jac.bin"))
     Jr = fm.read_jac(gpath(name + "_jac.bin"))
@@ -66,8 +67,12 @@ def test_cli_qt_correct_equals_merged_db_block(tmp_path):
     assert np.array_equal(QM, AM[np.ix_(rows, cols)])
 
 
+@pytest.mark.parametrize("devs", [[], ["--devices", "0,0,0"]], ids=["1dev", "3ctx"])
 @pytest.mark.parametrize("case", ["all48", "qsub40", "qt12"])
-def test_cli_vs_reference_binary_on_syn(tmp_path, case):
+def test_cli_vs_reference_binary_on_syn(tmp_path, case, devs):
+    """The CLI's CSV equals the reference binary's, on one context and with the
+    rows split over three contexts (--devices 0,0,0: the multi-GPU path, one
+    host thread per context, on the box's one GPU; -q runs on the first)."""
     import make_ref_vectors as mk
     kind, kw = mk.CASES[case]
     kw = dict(kw)
@@ -75,21 +80,21 @@ def test_cli_vs_reference_binary_on_syn(tmp_path, case):
     if kind == "all":
         db = str(tmp_path / "s.db")
         syn.write_db(db, **kw)
-        run(db, out)
+        run(db, out, *devs)
     elif kind == "qsub":
         query = kw.pop("query")
         db = str(tmp_path / "s.db")
         g = syn.write_db(db, **kw)
         ql = tmp_path / "q.txt"
         ql.write_text("\n".join(g["genome_set"][i] for i in query) + "\n")
-        run(db, out, "-q", str(ql))
+        run(db, out, "-q", str(ql), *devs)
     else:
         nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")
         tdb, qdb = str(tmp_path / "t.db"), str(tmp_path / "q.db")
         syn.write_db(tdb, n_genomes=nT, **kw)
         syn.write_db(qdb, n_genomes=nQ, genome_prefix="qry", genome_seed=syn.DEFAULT_SEED + 1,
                      n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
-        run(tdb, out, "-r", qdb, "--ref-compat")
+        run(tdb, out, "-r", qdb, "--ref-compat", *devs)
     assert open(out).read() == text(f"ref_{case}.csv")
 
 

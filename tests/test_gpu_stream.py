@@ -161,3 +161,27 @@ def test_column_windows_equal_row_chunks(engine, monkeypatch, mode):
                                            flags | _capi.FLAG_EMIT_JAC)
             assert nt > 1 and ne3 == ne1
             assert np.array_equal(a3, a1) and np.array_equal(S3, S1) and np.array_equal(N3, N1)
+
+
+def test_compute_rows_two_contexts_fill_one_array(engine):
+    """pfaai_compute_rows: two contexts (here both on device 0) each write
+    their row block's JAC span of one host array; == pfaai_compute."""
+    from parfastaai_amd.shard import split_rows
+
+    pb = _all_problem(700, 30, clade_size=10)
+    engine.load(**pb)
+    ref_a, ref_S, ref_N = engine.compute(0)
+    e2 = _capi.Engine(0)
+    try:
+        e2.load(**pb)
+        n = len(ref_a)
+        a = np.full(n, np.nan)
+        S = np.full(n, np.nan)
+        N = np.full(n, -1, np.int32)
+        (r0, r1), (r2, r3) = split_rows(700, 2)
+        for e, (rb, re) in ((engine, (r0, r1)), (e2, (r2, r3))):
+            rc = e.lib.pfaai_compute_rows(e.ctx, rb, re, 0, a.ctypes.data, S.ctypes.data, N.ctypes.data)
+            e._check(rc, "pfaai_compute_rows")
+        assert np.array_equal(a, ref_a) and np.array_equal(S, ref_S) and np.array_equal(N, ref_N)
+    finally:
+        e2.close()
