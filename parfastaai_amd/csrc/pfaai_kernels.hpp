@@ -328,10 +328,13 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
     if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
     __syncthreads();
     const int64_t S = lp[0], E = lp[nt];
-    auto tet_of = [&](int64_t i) {  // tetramer of F entry i within the tile
-        int tl = 0;
-        while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
-        return tl;
+    auto tet_of = [&](int64_t i) {  // tetramer of F entry i within the tile: last tl with lp[tl] <= i
+        int lo = 0, hi = nt - 1;       // binary search over <= 16 block starts (was a linear scan)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lp[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        return lo;
     };
     // (1) F is sorted by (tetramer, protein, genome): a run starts where the
     // protein changes and ends where it changes again -- each protein has one
@@ -364,6 +367,7 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
         if (!in) continue;
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
         int tl = tet_of(max(c0, S));
+        int64_t cur = lp[tl], nb = lp[tl + 1];  // block [cur, nb) of tetramer tl, kept in registers
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int64_t i = c0 + j;
@@ -371,8 +375,12 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
             const uint32_t qp = j == 0 ? prev : (w[(j - 1) >> 1] >> (16 * ((j - 1) & 1))) & 0xFFFFu;
             const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
             if (i < S || i >= E) continue;
-            while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
-            bool head = i == lp[tl] || qp != q, tail = i + 1 == lp[tl + 1] || qn != q;
+            if (i >= nb) {  // crossed into a later tetramer block (rare: blocks hold ~1800 entries)
+                while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
+                cur = lp[tl];
+                nb = lp[tl + 1];
+            }
+            bool head = i == cur || qp != q, tail = i + 1 == nb || qn != q;
             int wo = 0;  // window table offset
             if constexpr (WIN) {  // sub-runs by window: ids ascend along a run
                 const int32_t g = gg[j], gp = j == 0 ? gprev : gg[j - 1], gn = j == 7 ? gnext : gg[j + 1];
