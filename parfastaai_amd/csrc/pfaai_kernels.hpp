@@ -316,7 +316,9 @@ __device__ __forceinline__ int32_t win_of(int32_t g, int32_t wcols, float inv) {
 template <bool WIN = false, int NTH = kTetraThreads>
 __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wcols = 0,
                                                        int32_t nwin = 1) {
-    extern __shared__ uint4 ent[];  // [nwin][n_prot][kBlkTile] runs of the tile's tetramers
+    // [nwin][kBlkTile][n_prot]: tetramer-major in LDS, so the heads / tails of
+    // one tetramer's runs (consecutive proteins) land in different banks
+    extern __shared__ uint4 ent[];
     __shared__ int64_t lp[kBlkTileMax + 1];
     const int tid = threadIdx.x, P = d.n_prot;
     const int t0 = blockIdx.x * kBlkTile;
@@ -389,8 +391,8 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
                 tail = tail || gn >= (w + 1) * wcols;
                 wo = w * PW;
             }
-            if (head) ent[wo + q * kBlkTile + tl].x = (uint32_t)i;
-            if (tail) ent[wo + q * kBlkTile + tl].y = (uint32_t)(i + 1);
+            if (head) ent[wo + tl * P + q].x = (uint32_t)i;
+            if (tail) ent[wo + tl * P + q].y = (uint32_t)(i + 1);
         }
     }
     __syncthreads();
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + (int64_t)u * NTH * kGroup;
             if (i >= E) continue;
-            uint4* r = &ent[(WIN ? win_of((int32_t)g[u], wcols, inv) * PW : 0) + q[u] * kBlkTile + tet_of(i)];
+            uint4* r = &ent[(WIN ? win_of((int32_t)g[u], wcols, inv) * PW : 0) + tet_of(i) * P + q[u]];
             const uint32_t k = (uint32_t)(i - (r->x & ~(uint32_t)(kGroup - 1))) / kGroup;  // line of the run
             if (k < 1 || k > (uint32_t)kSplitters) continue;
             const uint64_t field = ~(kSplitNone << (kSplitBits * (k - 1))) | ((uint64_t)g[u] << (kSplitBits * (k - 1)));
@@ -424,7 +426,8 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
     // (3) write out: consecutive entries of one protein (and window) per tile
     for (int k = tid; k < (WIN ? nwin : 1) * PW && !(dbg & 4); k += NTH) {
         const int tl = k % kBlkTile;
-        if (tl < nt) d.blk[(int64_t)(k / kBlkTile) * kNTetramers + t0 + tl] = ent[k];
+        const int wq = k / kBlkTile;  // w * P + q: global writes stay 16 consecutive tetramers of one protein
+        if (tl < nt) d.blk[(int64_t)wq * kNTetramers + t0 + tl] = ent[(wq / P) * PW + tl * P + wq % P];
     }
 }
 
