@@ -824,6 +824,13 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         c->rows_kernel = k;
     }
     if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
+    // k_rows_pl wave priorities: bit 0 raises the load-issue stages above other
+    // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33
+    // ms at 10k, tools/gpu/ab_rows.py); PFAAI_PL_PRIO=0..3 overrides (A/B)
+    {
+        const char* pr = getenv("PFAAI_PL_PRIO");
+        flags = (flags & ~(3u << 16)) | (uint32_t)((pr ? atoi(pr) : 3) & 3) << 16;
+    }
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
         HIPCHK(c, hipStreamSynchronize(s));
         c->pool_used = 0;

@@ -140,6 +140,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int32_t ncw = (whi - cc0 + 1) >> 1;
     const bool compat = flags & 1u;
     const uint32_t min_len = abs_chunk >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
+    const uint32_t prio = (flags >> 16) & 3u;
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
@@ -263,6 +264,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // T(i-1): T16 words of the thread's columns and T[p][A], issued
         // first so that S5 waits for nothing issued after them
         const int pt = i >= 1 ? i - 1 : 0;
+        if (prio & 1u) __builtin_amdgcn_s_setprio(2);  // loads issue ahead of other waves' S5 (flags bits 16-17)
         uint32_t tw[KW];
         const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
 #pragma unroll
@@ -279,6 +281,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         s2(i + 2, gt, r4);
         s1(i + 3, gt);
         stamp(2);
+        if (prio) __builtin_amdgcn_s_setprio(0);
         // S5: normalise protein i-1 (fp64, ascending protein order per pair)
         if (has_p) {
             uint32_t* acc_p = acc + (st ^ 1) * W;
@@ -305,6 +308,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             }
         }
         stamp(3);
+        if (prio & 2u) __builtin_amdgcn_s_setprio(1);
         // S4b: atomics of the first round, further rounds (two tasks per
         // group in flight), whole-workgroup runs
         if (has_i) {
