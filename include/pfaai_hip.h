@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PFAAI_ABI_VERSION 2
+#define PFAAI_ABI_VERSION 3 /* 3: pfaai_build_f, pfaai_compute_rows, pfaai_stream, KEEP_RUNS */
 #define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
 
 /* Error codes: 0..3 mirror PFAAI_ERROR_CODE (interface.hpp:39-44). */
@@ -168,7 +168,8 @@ int pfaai_stream(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, int64_t til
 /* |E| summed over the tiles of the last pfaai_stream. */
 int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 
-/* Rows [row_begin, row_end) into HOST arrays of length n_pairs indexed by
+/* ParFAAIImpl::run() (algorithm_impl.hpp:325-329) for a block of rows:
+ * rows [row_begin, row_end) into HOST arrays of length n_pairs indexed by
  * the JAC index (only the rows' entries are written; any may be NULL).
  * Synchronous.  ALL and QT: disjoint row blocks have disjoint spans, so one
  * host thread per context (one context per device) fills a shared host
