@@ -823,6 +823,10 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
             k = RK_FUSED;
         c->rows_kernel = k;
     }
+    {  // consecutive rows per XCD (L2 sharing of a clade's runs); PFAAI_XCD_CHUNK for A/B
+        const char* xc = getenv("PFAAI_XCD_CHUNK");
+        c->dev.xcd_chunk = xc ? std::max(1, atoi(xc)) : kXcdChunk;
+    }
     if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
     // k_rows_pl wave priorities: bit 0 raises the load-issue stages above other
     // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33

@@ -65,6 +65,7 @@ struct Dev {
     const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)
     const uint16_t* T16c;       // same through tcol_col (ref-compat QT quirk); == T16 otherwise
     int64_t t16_cols;           // even, >= n_ids
+    int32_t xcd_chunk;          // consecutive rows per XCD in xcd_row (PFAAI_XCD_CHUNK, default kXcdChunk)
 };
 
 // XCD-aware row order (MI355X_MICROARCH.md: workgroups are dealt round-robin
@@ -77,11 +78,11 @@ struct Dev {
 constexpr int kXcds = 8;
 constexpr int kXcdChunk = 32;
 
-__device__ __forceinline__ int64_t xcd_row(int64_t b, int64_t n) {
-    const int64_t full = (n / (kXcds * kXcdChunk)) * (kXcds * kXcdChunk);
+__device__ __forceinline__ int64_t xcd_row(int64_t b, int64_t n, int64_t ch = kXcdChunk) {
+    const int64_t full = (n / (kXcds * ch)) * (kXcds * ch);
     if (b >= full) return b;
     const int64_t x = b % kXcds, i = b / kXcds;
-    return (i / kXcdChunk) * (kXcds * kXcdChunk) + x * kXcdChunk + (i % kXcdChunk);
+    return (i / ch) * (kXcds * ch) + x * ch + (i % ch);
 }
 
 // ---------------------------------------------------------------------------

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int grp = tid >> 2, gl = tid & 3;
-    const int64_t rl = xcd_row(blockIdx.x, gridDim.x);
+    const int64_t rl = xcd_row(blockIdx.x, gridDim.x, d.xcd_chunk);
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
     row_cols<MODE>(d, a, clo, chi);
