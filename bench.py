@@ -265,7 +265,8 @@ def main():
             "config": {"workload": f"SYN all-vs-all N={args.genomes} P={args.prot} (BASELINE configs[2] DB; "
                                    f"row-block sharded, RCCL gather to rank 0)",
                        "genomes": args.genomes, "proteins": args.prot, "pairs": n_pairs, "F": n_f,
-                       "events": total_events, "parallelism": f"rowblock{world}",
+                       "events": total_events, "events_per_s": round(total_events / (ms_per_step * 1e-3), 1),
+                       "parallelism": f"rowblock{world}",
                        "hot_path_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                        "k_rows_ms_max_rank": round(k_rows_ms_max, 4),
                        "k_build_ms_max_rank": round(k_build_ms_max, 4)},
