@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -152,6 +154,22 @@ int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
 }
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Host-side checks of pfaai_load over |F|-sized arrays: [0, n) split over up
+// to 16 threads, one per 2^20 units of `work` (default n): fn(lo, hi, thread).
+template <class Fn>
+int par_for(int64_t n, Fn fn, int64_t work = -1) {
+    const int64_t hw = std::max<int64_t>(1, (int64_t)std::thread::hardware_concurrency());
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({hw, 16, (work < 0 ? n : work) >> 20, n}));
+    if (nt == 1) {
+        fn((int64_t)0, n, 0);
+        return 1;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt, t); });
+    for (auto& x : th) x.join();
+    return nt;
+}
 
 // exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
@@ -691,18 +709,22 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
             if (p.G_off[k + 1] < p.G_off[k]) return fail(c, PFAAI_ERR_INVALID, "G_off must be non-decreasing");
         const int64_t gt = p.G_off[ng];
         if (gt >= ((int64_t)1 << 32)) return fail(c, PFAAI_ERR_INVALID, "G too large");
-        for (int64_t k = 0; k < gt; ++k)
-            if (p.G_tet[k] < 0 || p.G_tet[k] >= PFAAI_NTETRAMERS)
-                return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
+        std::atomic<int> bad_g{0};
+        par_for(gt, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k)
+                if (p.G_tet[k] < 0 || p.G_tet[k] >= PFAAI_NTETRAMERS) { bad_g = 1; return; }
+        });
+        if (bad_g) return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
         c->max_glen = 0;
         for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, p.G_off[k + 1] - p.G_off[k]);
         if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
         if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
         // u16 protein ids of F for k_blk's run detection (n_prot < 4096)
-        std::vector<uint16_t> fp16((size_t)p.n_f);
-        for (int64_t i = 0; i < p.n_f; ++i) fp16[i] = (uint16_t)p.F_prot[i];
-        fp16.resize((size_t)p.n_f + 16, 0);  // 16-B reads may pass the end
+        std::vector<uint16_t> fp16((size_t)p.n_f + 16, 0);  // 16-B reads may pass the end
+        par_for(p.n_f, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t i = lo; i < hi; ++i) fp16[i] = (uint16_t)p.F_prot[i];
+        });
         if ((rc = upload(c, c->Fp16, fp16.data(), fp16.size()))) return rc;
     }
 
@@ -736,19 +758,37 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     // Work-list entries of a row = F entries of its genome (counted here).
     {
         std::vector<int64_t> fcount(ni, 0);
-        for (int64_t i = 0; i < p.n_f; ++i) {
-            const int32_t g = p.F_genome[i];
-            if (g < 0 || g >= ni) return fail(c, PFAAI_ERR_INVALID, "F holds a genome id outside [0, n_ids)");
-            if (p.F_prot[i] < 0 || p.F_prot[i] >= p.n_prot)
-                return fail(c, PFAAI_ERR_INVALID, "F holds a protein id outside [0, n_prot)");
-            fcount[g]++;
-        }
+        std::vector<std::vector<int64_t>> fc(16);
+        std::atomic<int> bad_id{0}, bad_p{0}, bad_sort{0};
+        const int nth = par_for(p.n_f, [&](int64_t lo, int64_t hi, int t) {
+            std::vector<int64_t>& cnt = fc[t];
+            cnt.assign(ni, 0);
+            for (int64_t i = lo; i < hi; ++i) {
+                const int32_t g = p.F_genome[i];
+                if (g < 0 || g >= ni) { bad_id = 1; return; }
+                if (p.F_prot[i] < 0 || p.F_prot[i] >= p.n_prot) { bad_p = 1; return; }
+                cnt[g]++;
+            }
+        });
+        if (bad_id) return fail(c, PFAAI_ERR_INVALID, "F holds a genome id outside [0, n_ids)");
+        if (bad_p) return fail(c, PFAAI_ERR_INVALID, "F holds a protein id outside [0, n_prot)");
+        for (int t = 0; t < nth; ++t)
+            for (int32_t g = 0; g < ni; ++g) fcount[g] += fc[t][g];
         // F sorted by (tetramer, protein, genome) -- ds_helper.hpp:126-162; the
-        // run table and the line pruning rely on it
-        for (int t = 0; t < PFAAI_NTETRAMERS; ++t)
-            for (int64_t i = p.Lp[t] + 1; i < p.Lp[t + 1]; ++i)
-                if (p.F_prot[i] < p.F_prot[i - 1] || (p.F_prot[i] == p.F_prot[i - 1] && p.F_genome[i] <= p.F_genome[i - 1]))
-                    return fail(c, PFAAI_ERR_INVALID, "F must be sorted by (tetramer, protein, genome)");
+        // run table and the line pruning rely on it (checked by tetramer blocks)
+        par_for(
+            PFAAI_NTETRAMERS,
+            [&](int64_t lo, int64_t hi, int) {
+                for (int64_t t = lo; t < hi; ++t)
+                    for (int64_t i = p.Lp[t] + 1; i < p.Lp[t + 1]; ++i)
+                        if (p.F_prot[i] < p.F_prot[i - 1] ||
+                            (p.F_prot[i] == p.F_prot[i - 1] && p.F_genome[i] <= p.F_genome[i - 1])) {
+                            bad_sort = 1;
+                            return;
+                        }
+            },
+            p.n_f);
+        if (bad_sort) return fail(c, PFAAI_ERR_INVALID, "F must be sorted by (tetramer, protein, genome)");
         c->row_fprefix.assign(c->n_rows + 1, 0);
         for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
         if (c->has_g) {  // work lists follow G (one record per G entry of a row genome)
