@@ -14,7 +14,12 @@
  * Conventions
  *   - return 0 on success; 1..3 are the reference's PFAAI_ERROR_CODE values
  *     (interface.hpp:39-44), 4..7 are new (HIP runtime, device OOM, RCCL,
- *     invalid argument).  pfaai_last_error() gives a message.
+ *     invalid argument).  pfaai_last_error() gives a message.  The names
+ *     carry a PFAAI_RC_ prefix so that this header can be included next to
+ *     the reference's interface.hpp, whose enum PFAAI_ERROR_CODE already
+ *     defines PFAAI_OK / PFAAI_ERR_SQLITE_DB / _SQLITE_MEM_ALLOC / _CONSTRUCT
+ *     with the same values.
+ *   - no C++ exception crosses the ABI (allocation failures -> PFAAI_RC_OOM).
  *   - host inputs are borrowed for the duration of the call; device buffers
  *     are owned by the context; outputs are caller-owned.
  *   - one host thread drives one context; a context owns one device.
@@ -28,19 +33,20 @@
 extern "C" {
 #endif
 
-#define PFAAI_ABI_VERSION 3 /* 3: pfaai_build_f, pfaai_compute_rows, pfaai_stream, KEEP_RUNS */
+#define PFAAI_ABI_VERSION 4 /* 4: F or G built on the device at load, pfaai_run_info,
+                                 PFAAI_RC_* names, dense row matrices (pfaai_stream_matrix) */
 #define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
 
-/* Error codes: 0..3 mirror PFAAI_ERROR_CODE (interface.hpp:39-44). */
+/* Error codes: 0..3 have PFAAI_ERROR_CODE's values (interface.hpp:39-44). */
 enum {
-    PFAAI_OK = 0,
-    PFAAI_ERR_SQLITE_DB = 1,
-    PFAAI_ERR_SQLITE_MEM_ALLOC = 2,
-    PFAAI_ERR_CONSTRUCT = 3,
-    PFAAI_ERR_HIP = 4,
-    PFAAI_ERR_OOM = 5,
-    PFAAI_ERR_RCCL = 6,
-    PFAAI_ERR_INVALID = 7
+    PFAAI_RC_OK = 0,
+    PFAAI_RC_SQLITE_DB = 1,
+    PFAAI_RC_SQLITE_MEM_ALLOC = 2,
+    PFAAI_RC_CONSTRUCT = 3,
+    PFAAI_RC_HIP = 4,
+    PFAAI_RC_OOM = 5,
+    PFAAI_RC_RCCL = 6,
+    PFAAI_RC_INVALID = 7
 };
 
 /* Modes: which genome pairs are valid and how they index the JAC array.
@@ -55,6 +61,11 @@ enum { PFAAI_MODE_ALL = 0, PFAAI_MODE_QSUB = 1, PFAAI_MODE_QT = 2 };
 #define PFAAI_FLAG_KEEP_RUNS 4u  /* reuse the run table an earlier pfaai_run on this
                                     load built (same stream or ordered after it):
                                     row tiles / pipelined shards pay k_blk once */
+
+/* Row kernels (pfaai_run_info): k_rows_pl (genome-major walk, the default),
+ * its 512-thread form, the fused k_rows (G lists > 1024 entries), and the
+ * work-list k_rows (no genome-major view could be formed). */
+enum { PFAAI_ROWS_PL = 0, PFAAI_ROWS_PL512 = 1, PFAAI_ROWS_FUSED = 2, PFAAI_ROWS_WORKLIST = 3 };
 
 typedef struct pfaai_ctx pfaai_ctx;
 
@@ -71,10 +82,14 @@ typedef struct {
     int32_t t_cols;        /* columns of T (T is P x t_cols, row-major) */
     int32_t n_qry;         /* QSUB: |query list|; QT: genomes of the query DB */
     int32_t n_tgt;         /* QSUB: n_ids - n_qry; QT: genomes of the target DB; ALL: unused */
-    int64_t n_f;           /* |F| (<= 2^32 - 64) */
+    int64_t n_f;           /* |F| (<= 2^32 - 64); ignored when F is built from G */
     const int64_t* Lp;     /* [PFAAI_NTETRAMERS + 1] exclusive prefix of Lc, Lp[160000] = n_f */
     const int32_t* F_prot; /* [n_f] F[i].first  (protein index) */
-    const int32_t* F_genome; /* [n_f] F[i].second (genome id) */
+    const int32_t* F_genome; /* [n_f] F[i].second (genome id)
+                              * Lp, F_prot and F_genome may all be NULL when
+                              * G_off / G_tet are given: F is then built on the
+                              * device from G (stable radix sort by tetramer *
+                              * n_prot + protein, ds_helper.hpp:126-162). */
     const int32_t* T;      /* [n_prot * t_cols] T(p, g) tetramer counts */
     const uint8_t* is_q;   /* [n_ids] QSUB/QT: 1 for query genomes (NULL for ALL) */
     const int32_t* q_index; /* [n_ids] QSUB: position of the genome in the query file, -1 otherwise */
@@ -85,9 +100,13 @@ typedef struct {
      * G_tet[G_off[g*n_prot+p] .. G_off[g*n_prot+p+1]), ascending.  With it
      * the row kernel walks genome g's tetramer list directly and looks each
      * (protein, tetramer) run of F up in a dense run table built once per
-     * run (no sort, no per-step work lists); without it the rows are fed
-     * from work lists built from F alone (PFAAI_ROWS_KERNEL=worklist).
-     * Entries whose tetramer block is absent from F are ignored. */
+     * run (no sort, no per-step work lists).  When G is NULL, pfaai_load
+     * builds it on the device from F (stable radix sort of the F entries by
+     * genome * n_prot + protein), so F-only callers -- the reference's own
+     * DataStructInterface classes -- run the same kernels.  When both F and
+     * G are given, G must list exactly the memberships of F (checked on the
+     * device: every G entry's genome is found in its run of F, |G| == |F|,
+     * lists strictly ascending). */
     const int64_t* G_off;  /* [n_ids * n_prot + 1] */
     const int32_t* G_tet;  /* [G_off[n_ids * n_prot]] */
 } pfaai_problem;
@@ -177,6 +196,10 @@ int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
  * adapter's multi-device constructor).  QSUB: all rows only. */
 int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
                        double* h_aji, double* h_S, int32_t* h_N);
+
+/* Which row kernel the last pfaai_run launched (PFAAI_ROWS_*) and whether it
+ * ran by absolute column windows (rows wider than one kernel chunk). */
+int pfaai_run_info(const pfaai_ctx* ctx, int32_t* rows_kernel, int32_t* column_windows);
 
 /* |E| of the last run, counted by the scatter kernel (equals the reference's
  * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and

@@ -7,20 +7,36 @@
 //   int computeAJI();  const std::vector<JACType>& getJAC() const;
 //   const std::vector<ValueType>& getAJI() const;
 // DSIT is any type with the reference's DataStructInterface accessors
-// (interface.hpp:200-328): refLp(), refLc(), refF() (elements with .first/
-// .second), refT() (operator()(p, g), rows(), cols()), initJAC(),
-// nGenomePairs(), qrySetSize(), tgtSetSize(), isQryGenome(), mapQueryId(),
-// plus the JACType typedef -- the reference's own ParFAAIData /
-// ParFAAIQSubData / ParFAAIQryTgtData qualify unchanged, and so do the host
-// classes of parfastaai_amd/host/datastruct.hpp.  The mode is deduced from the
-// DSIT (pfaai_mode_of<DSIT>) or passed explicitly.
+// (interface.hpp:200-328): refLc(), refF() (elements with .first/.second),
+// refT() (operator()(p, g), rows(), cols()), initJAC(), qrySetSize(),
+// tgtSetSize(), isQryGenome(), mapQueryId(), plus the JACType typedef -- the
+// reference's own ParFAAIData / ParFAAIQSubData / ParFAAIQryTgtData qualify
+// unchanged, and so do the host classes of parfastaai_amd/host/datastruct.hpp.
+// A DSIT that also holds the genome-major `<p>_genomes` lists (refGOff(),
+// refGTet()) hands them over too; with an empty refF() only G is sent and F
+// is built on the device.
+//
+// The mode is deduced from the DSIT (pfaai_mode_of<DSIT>, specialisable):
+// a type with nUnionGenomes() is query-vs-target (ParFAAIQryTgtData,
+// ds_impl.hpp:370); otherwise the index maps decide -- every genome a query
+// under the identity map is all-vs-all (ParFAAIData, ds_impl.hpp:83-96),
+// anything else the query subset (ParFAAIQSubData, ds_impl.hpp:251-276).
+//
+// The one-argument constructor is the drop-in: it reproduces the class it
+// replaces bit for bit, quirks included (PFAAI_FLAG_REF_COMPAT: SURVEY 8a
+// rows Z and Q).  The explicit forms choose the mode, the corrected
+// semantics (ref_compat = false) and the device(s).
 #pragma once
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
-#include <thread>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <system_error>
+#include <thread>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "pfaai_hip.h"
@@ -32,38 +48,95 @@ struct HipError : std::runtime_error {
     HipError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+namespace detail {
+template <class T, class = void>
+struct has_union_genomes : std::false_type {};
+template <class T>
+struct has_union_genomes<T, std::void_t<decltype(std::declval<const T&>().nUnionGenomes())>> : std::true_type {};
+template <class T, class = void>
+struct has_genome_major : std::false_type {};
+template <class T>
+struct has_genome_major<T, std::void_t<decltype(std::declval<const T&>().refGOff()),
+                                       decltype(std::declval<const T&>().refGTet())>> : std::true_type {};
+
+struct CtxDeleter {
+    void operator()(pfaai_ctx* c) const { pfaai_destroy(c); }
+};
+using CtxPtr = std::unique_ptr<pfaai_ctx, CtxDeleter>;
+
+inline CtxPtr make_ctx(int device) {
+    pfaai_ctx* c = nullptr;
+    const int rc = pfaai_create(&c, device);
+    if (rc) throw HipError(rc, "pfaai_create failed for device " + std::to_string(device) + " (no visible MI355X?)");
+    return CtxPtr(c);
+}
+
+// [0, n) over up to 16 host threads (the adapter's array conversions)
+template <class Fn>
+void par_range(int64_t n, Fn fn) {
+    const int nt = (int)std::max<int64_t>(
+        1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 22}));
+    std::vector<std::thread> th;
+    int started = 0;
+    try {
+        for (; started < nt; ++started) th.emplace_back([&, t = started] { fn(n * t / nt, n * (t + 1) / nt); });
+    } catch (const std::system_error&) {
+        for (int t = started; t < nt; ++t) fn(n * t / nt, n * (t + 1) / nt);
+    }
+    for (auto& x : th) x.join();
+}
+}  // namespace detail
+
+// Mode of a DSIT (see the header comment); specialise for other types.
+// Works through the abstract DataStructInterface too (the reference's
+// PFDSInterface, main.cpp:48): a query-vs-target DSIT numbers its queries
+// after its nT targets (ds_impl.hpp:381-383), so none of ids [0, nT) is a
+// query; a query subset marks exactly its nQ queries among all genomes
+// (ds_impl.hpp:230-232); all-vs-all marks every genome, identity map.
+template <class DSIT>
+struct pfaai_mode_of {
+    static int deduce(const DSIT& ds) {
+        if constexpr (detail::has_union_genomes<DSIT>::value) {
+            return PFAAI_MODE_QT;
+        } else {
+            const int64_t nq = (int64_t)ds.qrySetSize(), n = (int64_t)ds.tgtSetSize();
+            int64_t marked = 0;
+            bool identity = true;
+            for (int64_t g = 0; g < n; ++g) {
+                if (!ds.isQryGenome((decltype(ds.qrySetSize()))g)) continue;
+                ++marked;
+                identity = identity && (int64_t)ds.mapQueryId((decltype(ds.qrySetSize()))g) == g;
+            }
+            if (marked != nq) return PFAAI_MODE_QT;
+            return (nq == n && identity) ? PFAAI_MODE_ALL : PFAAI_MODE_QSUB;
+        }
+    }
+};
+
 template <typename IdType, typename ValueType, typename DSIT>
 class ParFAAIHipImpl {
   public:
     using JACType = typename DSIT::JACType;
 
+    // the drop-in: ParFAAIImpl(const DSIT&) (algorithm_impl.hpp:75-79), mode
+    // deduced, reference-exact (ref_compat), device 0
+    explicit ParFAAIHipImpl(const DSIT& ds)
+        : ParFAAIHipImpl(ds, pfaai_mode_of<DSIT>::deduce(ds), std::vector<int>{0}, true) {}
     // mode: PFAAI_MODE_ALL / QSUB / QT (the three reference DSIT classes)
-    explicit ParFAAIHipImpl(const DSIT& ds, int mode, int device = 0, bool ref_compat = false)
-        : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
-        int rc = pfaai_create(&m_ctx, device);
-        if (rc) throw HipError(rc, "pfaai_create failed (no visible MI355X?)");
-        upload();
-    }
+    ParFAAIHipImpl(const DSIT& ds, int mode, int device = 0, bool ref_compat = false)
+        : ParFAAIHipImpl(ds, mode, std::vector<int>{device}, ref_compat) {}
     // Multi-GPU (one process, one context per device, one host thread per
     // context): rows are split by the row-cost model of parfastaai_amd/shard.py
     // and every device writes its rows' JAC span of the shared host arrays
     // (pfaai_compute_rows); ALL and QT -- QSUB runs on devices[0].
     ParFAAIHipImpl(const DSIT& ds, int mode, const std::vector<int>& devices, bool ref_compat = false)
         : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
-        if (devices.empty()) throw HipError(PFAAI_ERR_INVALID, "no device");
-        int rc = pfaai_create(&m_ctx, devices[0]);
-        if (rc) throw HipError(rc, "pfaai_create failed (no visible MI355X?)");
-        for (std::size_t i = 1; i < devices.size() && mode != PFAAI_MODE_QSUB; ++i) {
-            pfaai_ctx* x = nullptr;
-            rc = pfaai_create(&x, devices[i]);
-            if (rc) throw HipError(rc, "pfaai_create failed for device " + std::to_string(devices[i]));
-            m_extra.push_back(x);
-        }
+        if (devices.empty()) throw HipError(PFAAI_RC_INVALID, "no device");
+        // contexts are owned by RAII handles: a throw below releases them
+        m_ctx.push_back(detail::make_ctx(devices[0]));
+        for (std::size_t i = 1; i < devices.size() && mode != PFAAI_MODE_QSUB; ++i)
+            m_ctx.push_back(detail::make_ctx(devices[i]));
         upload();
-    }
-    ~ParFAAIHipImpl() {
-        pfaai_destroy(m_ctx);
-        for (pfaai_ctx* x : m_extra) pfaai_destroy(x);
     }
     ParFAAIHipImpl(const ParFAAIHipImpl&) = delete;
     ParFAAIHipImpl& operator=(const ParFAAIHipImpl&) = delete;
@@ -84,9 +157,9 @@ class ParFAAIHipImpl {
         std::vector<int32_t> N(n);
         m_AJIdev.resize(n);
         const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
-        if (m_extra.empty()) {
-            int rc = pfaai_compute(m_ctx, flags, m_AJIdev.data(), S.data(), N.data());
-            if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        if (m_ctx.size() == 1) {
+            int rc = pfaai_compute(ctx(), flags, m_AJIdev.data(), S.data(), N.data());
+            if (rc) throw HipError(rc, pfaai_last_error(ctx()));
         } else {
             computeMulti(flags, S.data(), N.data());
         }
@@ -94,7 +167,10 @@ class ParFAAIHipImpl {
             m_JAC[i].S = S[i];
             m_JAC[i].N = N[i];
         }
-        if (m_extra.empty()) pfaai_last_stats(m_ctx, &m_events, &m_msBuild, &m_msRows);
+        if (m_ctx.size() == 1) {
+            pfaai_last_stats(ctx(), &m_events, &m_msBuild, &m_msRows);
+            pfaai_run_info(ctx(), &m_rowsKernel, nullptr);
+        }
         return 0;  // PFAAI_OK
     }
     // algorithm_impl.hpp:309-322 (the kernel epilogue already divided S / N)
@@ -116,33 +192,47 @@ class ParFAAIHipImpl {
     // QT modes.  Returns 0, or the engine / I/O error code.
     int streamAJI(const std::string& path, int64_t tile_pairs) {
         int64_t rows = 0, pairs = 0;
-        int rc = pfaai_shape(m_ctx, &rows, &pairs);
-        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
+        int rc = pfaai_shape(ctx(), &rows, &pairs);
+        if (rc) throw HipError(rc, pfaai_last_error(ctx()));
         FILE* f = std::fopen(path.c_str(), "wb");
-        if (!f) return PFAAI_ERR_INVALID;
+        if (!f) return PFAAI_RC_INVALID;
         const uint64_t n = (uint64_t)pairs;
         bool ok = std::fwrite(&n, 8, 1, f) == 1;
         auto sink = [](void* user, int64_t, int64_t, int64_t, int64_t count, const double* aji, const double*,
                        const int32_t*) -> int {
             return std::fwrite(aji, sizeof(double), (size_t)count, static_cast<FILE*>(user)) == (size_t)count
-                       ? 0 : PFAAI_ERR_INVALID;
+                       ? 0 : PFAAI_RC_INVALID;
         };
-        rc = ok ? pfaai_stream(m_ctx, 0, rows, tile_pairs, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, sink, f)
-                : PFAAI_ERR_INVALID;
+        rc = ok ? pfaai_stream(ctx(), 0, rows, tile_pairs, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, sink, f)
+                : PFAAI_RC_INVALID;
         ok = std::fclose(f) == 0 && ok;
-        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
-        pfaai_stream_events(m_ctx, &m_events);
-        return ok ? 0 : PFAAI_ERR_INVALID;
+        if (rc) throw HipError(rc, pfaai_last_error(ctx()));
+        pfaai_stream_events(ctx(), &m_events);
+        return ok ? 0 : PFAAI_RC_INVALID;
     }
     const std::vector<JACType>& getJAC() const { return m_JAC; }
     const std::vector<ValueType>& getAJI() const { return m_AJI; }
+    // the reference's debug listing (algorithm_impl.hpp:347-356; main.cpp
+    // calls it when NDEBUG is not defined)
+    void print_aji() const {
+        std::printf("AJI Ouput : \n [(GP1, GP2,   SUM, NCP) ->  AJI]\n");
+        for (std::size_t i = 0; i < m_JAC.size(); ++i)
+            std::printf(" [%lld, %.17g -> %03.2f] \n",
+                        (long long)m_ds.genomePairToIndex(m_JAC[i].genomeA, m_JAC[i].genomeB), (double)m_AJI[i],
+                        (double)m_AJI[i]);
+    }
     int64_t nEvents() const { return m_events; }
     float msBuild() const { return m_msBuild; }
     float msRows() const { return m_msRows; }
-
-    int nDevices() const { return 1 + (int)m_extra.size(); }
+    int mode() const { return m_mode; }
+    // PFAAI_ROWS_* of the last run
+    int rowsKernel() const { return m_rowsKernel; }
+    int nDevices() const { return (int)m_ctx.size(); }
+    pfaai_ctx* context() const { return ctx(); }
 
   private:
+    pfaai_ctx* ctx() const { return m_ctx.front().get(); }
+
     // contiguous row blocks balanced by the row-cost model (shard.py:split_rows)
     static std::vector<int64_t> splitRows(int64_t n, int parts, bool all_vs_all) {
         std::vector<int64_t> cut{0};
@@ -165,25 +255,24 @@ class ParFAAIHipImpl {
     }
     void computeMulti(uint32_t flags, double* S, int32_t* N) {
         int64_t rows = 0, pairs = 0;
-        pfaai_shape(m_ctx, &rows, &pairs);
-        std::vector<pfaai_ctx*> ctx{m_ctx};
-        ctx.insert(ctx.end(), m_extra.begin(), m_extra.end());
-        const auto cut = splitRows(rows, (int)ctx.size(), m_mode == PFAAI_MODE_ALL);
-        std::vector<int> rcs(ctx.size(), 0);
+        pfaai_shape(ctx(), &rows, &pairs);
+        const auto cut = splitRows(rows, (int)m_ctx.size(), m_mode == PFAAI_MODE_ALL);
+        std::vector<int> rcs(m_ctx.size(), 0);
         std::vector<std::thread> th;
-        for (std::size_t i = 0; i < ctx.size(); ++i)
+        for (std::size_t i = 0; i < m_ctx.size(); ++i)
             th.emplace_back([&, i] {
-                rcs[i] = pfaai_compute_rows(ctx[i], cut[i], cut[i + 1], flags, m_AJIdev.data(), S, N);
+                rcs[i] = pfaai_compute_rows(m_ctx[i].get(), cut[i], cut[i + 1], flags, m_AJIdev.data(), S, N);
             });
         for (auto& t : th) t.join();
         m_events = 0;
         m_msBuild = m_msRows = 0.f;
-        for (std::size_t i = 0; i < ctx.size(); ++i) {
-            if (rcs[i]) throw HipError(rcs[i], pfaai_last_error(ctx[i]));
+        for (std::size_t i = 0; i < m_ctx.size(); ++i) {
+            if (rcs[i]) throw HipError(rcs[i], pfaai_last_error(m_ctx[i].get()));
             if (cut[i + 1] == cut[i]) continue;
             int64_t e = 0;
             float b = 0.f, r = 0.f;
-            pfaai_last_stats(ctx[i], &e, &b, &r);
+            pfaai_last_stats(m_ctx[i].get(), &e, &b, &r);
+            pfaai_run_info(m_ctx[i].get(), &m_rowsKernel, nullptr);
             m_events += e;
             m_msBuild = std::max(m_msBuild, b);
             m_msRows = std::max(m_msRows, r);
@@ -191,32 +280,40 @@ class ParFAAIHipImpl {
     }
 
     void upload() {
-        const auto& Lp32 = m_ds.refLp();
         const auto& Lc = m_ds.refLc();
         const auto& F = m_ds.refF();
         const auto& T = m_ds.refT();
         const int64_t nf = (int64_t)F.size();
-        m_Lp.assign(PFAAI_NTETRAMERS + 1, 0);
-        for (int t = 0; t < PFAAI_NTETRAMERS; ++t) m_Lp[t + 1] = m_Lp[t] + (int64_t)Lc[t];
-        (void)Lp32;
-        m_Fp.resize(nf);
-        m_Fg.resize(nf);
-        for (int64_t i = 0; i < nf; ++i) {
-            m_Fp[i] = F[i].first;
-            m_Fg[i] = F[i].second;
+        pfaai_problem pb{};
+        if constexpr (detail::has_genome_major<DSIT>::value) {
+            if (!m_ds.refGTet().empty() || nf == 0) {
+                pb.G_off = m_ds.refGOff().data();
+                pb.G_tet = m_ds.refGTet().data();
+            }
+        }
+        if (nf > 0 || !pb.G_off) {  // F in the reference's layout -> the ABI's columns
+            m_Lp.assign(PFAAI_NTETRAMERS + 1, 0);
+            for (int t = 0; t < PFAAI_NTETRAMERS; ++t) m_Lp[t + 1] = m_Lp[t] + (int64_t)Lc[t];
+            m_Fp.resize(nf);
+            m_Fg.resize(nf);
+            detail::par_range(nf, [&](int64_t lo, int64_t hi) {
+                for (int64_t i = lo; i < hi; ++i) {
+                    m_Fp[i] = F[i].first;
+                    m_Fg[i] = F[i].second;
+                }
+            });
+            pb.n_f = nf;
+            pb.Lp = m_Lp.data();
+            pb.F_prot = m_Fp.data();
+            pb.F_genome = m_Fg.data();
         }
         const int64_t P = (int64_t)T.rows(), C = (int64_t)T.cols();
         m_T.resize(P * C);
         for (int64_t p = 0; p < P; ++p)
             for (int64_t g = 0; g < C; ++g) m_T[p * C + g] = T(p, g);
-        pfaai_problem pb{};
         pb.mode = m_mode;
         pb.n_prot = (int32_t)P;
         pb.t_cols = (int32_t)C;
-        pb.n_f = nf;
-        pb.Lp = m_Lp.data();
-        pb.F_prot = m_Fp.data();
-        pb.F_genome = m_Fg.data();
         pb.T = m_T.data();
         if (m_mode == PFAAI_MODE_ALL) {
             pb.n_ids = (int32_t)m_ds.tgtSetSize();
@@ -243,17 +340,21 @@ class ParFAAIHipImpl {
             for (int32_t g = pb.n_tgt; g < pb.n_ids; ++g) m_isq[g] = 1;
             pb.is_q = m_isq.data();
         }
-        int rc = pfaai_load(m_ctx, &pb);
-        if (rc) throw HipError(rc, pfaai_last_error(m_ctx));
-        for (pfaai_ctx* x : m_extra)
-            if ((rc = pfaai_load(x, &pb))) throw HipError(rc, pfaai_last_error(x));
+        for (auto& c : m_ctx) {
+            const int rc = pfaai_load(c.get(), &pb);
+            if (rc) throw HipError(rc, pfaai_last_error(c.get()));
+        }
+        // the devices hold their own copies now
+        std::vector<int64_t>().swap(m_Lp);
+        std::vector<int32_t>().swap(m_Fp);
+        std::vector<int32_t>().swap(m_Fg);
+        std::vector<int32_t>().swap(m_T);
     }
 
     const DSIT& m_ds;
     int m_mode;
     bool m_compat;
-    pfaai_ctx* m_ctx = nullptr;
-    std::vector<pfaai_ctx*> m_extra;  // further devices (multi-GPU constructor)
+    std::vector<detail::CtxPtr> m_ctx;  // one per device; [0] drives single-device runs
     std::vector<int64_t> m_Lp;
     std::vector<int32_t> m_Fp, m_Fg, m_T, m_qidx, m_trank;
     std::vector<uint8_t> m_isq;
@@ -262,6 +363,7 @@ class ParFAAIHipImpl {
     std::vector<ValueType> m_AJI;
     int64_t m_events = 0;
     float m_msBuild = 0.f, m_msRows = 0.f;
+    int32_t m_rowsKernel = -1;
 };
 
 }  // namespace pfaai

@@ -33,8 +33,9 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f", "pfaai_compute_rows",
+    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info",
 ]
+ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist"}
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
 #          const double* S, const int32_t* N)   (pfaai_sink_fn)
@@ -95,6 +96,7 @@ def load_library():
         "pfaai_build_f": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
+        "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     }
@@ -137,21 +139,23 @@ class Engine:
             pass
 
     # -- problem ----------------------------------------------------------------
-    def load(self, *, mode, n_ids, n_prot, Lp, F_prot, F_genome, T, n_qry=0, n_tgt=0,
+    def load(self, *, mode, n_ids, n_prot, T, Lp=None, F_prot=None, F_genome=None, n_qry=0, n_tgt=0,
              is_q=None, q_index=None, t_rank=None, G_off=None, G_tet=None):
-        Lp = np.ascontiguousarray(Lp, dtype=np.int64)
-        F_prot = np.ascontiguousarray(F_prot, dtype=np.int32)
-        F_genome = np.ascontiguousarray(F_genome, dtype=np.int32)
+        """F (Lp, F_prot, F_genome) and/or G (G_off, G_tet): whichever is
+        missing is built on the device (pfaai_load)."""
+        Lp = None if Lp is None else np.ascontiguousarray(Lp, dtype=np.int64)
+        F_prot = None if F_prot is None else np.ascontiguousarray(F_prot, dtype=np.int32)
+        F_genome = None if F_genome is None else np.ascontiguousarray(F_genome, dtype=np.int32)
         T = np.ascontiguousarray(T, dtype=np.int32)
         is_q = None if is_q is None else np.ascontiguousarray(is_q, dtype=np.uint8)
         q_index = None if q_index is None else np.ascontiguousarray(q_index, dtype=np.int32)
         t_rank = None if t_rank is None else np.ascontiguousarray(t_rank, dtype=np.int32)
         G_off = None if G_off is None else np.ascontiguousarray(G_off, dtype=np.int64)
         G_tet = None if G_tet is None else np.ascontiguousarray(G_tet, dtype=np.int32)
-        assert Lp.shape == (NTETRAMERS + 1,)
+        assert Lp is None or Lp.shape == (NTETRAMERS + 1,)
         assert T.ndim == 2 and T.shape[0] == n_prot
         pb = Problem(mode=mode, n_ids=n_ids, n_prot=n_prot, t_cols=T.shape[1], n_qry=n_qry,
-                     n_tgt=n_tgt, n_f=F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
+                     n_tgt=n_tgt, n_f=0 if F_prot is None else F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
                      F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
                      t_rank=_ptr(t_rank), G_off=_ptr(G_off), G_tet=_ptr(G_tet))
         self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
@@ -232,7 +236,10 @@ class Engine:
         ne, mb, mr = ctypes.c_int64(), ctypes.c_float(), ctypes.c_float()
         self._check(self.lib.pfaai_last_stats(self.ctx, ctypes.byref(ne), ctypes.byref(mb), ctypes.byref(mr)),
                     "pfaai_last_stats")
-        return {"n_events": ne.value, "ms_build": mb.value, "ms_rows": mr.value}
+        rk, win = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.pfaai_run_info(self.ctx, ctypes.byref(rk), ctypes.byref(win)), "pfaai_run_info")
+        return {"n_events": ne.value, "ms_build": mb.value, "ms_rows": mr.value,
+                "rows_kernel": ROWS_KERNELS.get(rk.value, "?"), "column_windows": bool(win.value)}
 
     def timing(self, reset=True):
         """(n_runs, ms_build_total, ms_rows_total) of the runs since the last reset."""

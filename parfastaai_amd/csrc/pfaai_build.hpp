@@ -1,0 +1,100 @@
+// pfaai_build.hpp -- the two orientations of the SCP membership at load time.
+//
+// The SCP database stores every (tetramer, protein, genome) membership twice
+// (scp_db.hpp:37-55): `<p>_tetras` (tetramer -> genome list: F, ordered by
+// (tetramer, protein, genome), ds_helper.hpp:126-162) and `<p>_genomes`
+// (genome -> tetramer list: G, (genome, protein)-major, ascending tetramers).
+// The row kernels need both: G to walk a row genome's own tetramers, F for
+// the run of every (tetramer, protein).  Whichever one the caller holds, the
+// other is built here with the stable LSD radix sort of pfaai_kernels.hpp
+// (k_rs_hist / k_rs_scatter, 8-bit digits):
+//   G from F   key = genome * P + protein of each F entry, record (tetramer,
+//              genome); F is sorted by tetramer, so the stable sort leaves
+//              every (genome, protein) list in ascending tetramer order.
+//   F from G   key = tetramer * P + protein of each G entry, record (protein,
+//              genome); G is genome-major, so the stable sort leaves every
+//              (tetramer, protein) run in ascending genome order -- exactly
+//              the reference's F (the UNION ALL ... ORDER BY of
+//              scp_db.hpp:161-216).  Lc is counted on the way in.
+// When both are given, k_g_check proves they list the same memberships.
+#pragma once
+#include "pfaai_kernels.hpp"
+
+namespace pfaai {
+
+// G-from-F keys: one workgroup per tetramer block (grid-stride over blocks).
+__global__ __launch_bounds__(256) void k_gkeys_from_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
+                                                      const int32_t* __restrict__ Fg, int32_t P,
+                                                      uint32_t* __restrict__ keys, uint2* __restrict__ recs) {
+    for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
+        const int64_t e = Lp[t + 1];
+        for (int64_t i = Lp[t] + threadIdx.x; i < e; i += blockDim.x) {
+            const int32_t g = Fg[i];
+            keys[i] = (uint32_t)g * (uint32_t)P + (uint32_t)Fp[i];
+            recs[i] = make_uint2((uint32_t)t, (uint32_t)g);
+        }
+    }
+}
+
+// sorted (tetramer, genome) records -> G_tet
+__global__ void k_gtet_split(const uint2* __restrict__ recs, int64_t n, int32_t* __restrict__ G_tet) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        G_tet[i] = (int32_t)recs[i].x;
+}
+
+// F-from-G keys: one wave per (genome, protein) list, lanes over its entries.
+__global__ __launch_bounds__(256) void k_fkeys_from_g(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
+                                                      int64_t n_lists, int32_t P, uint32_t* __restrict__ keys,
+                                                      uint2* __restrict__ recs, uint32_t* __restrict__ lc) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t L = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); L < n_lists; L += waves) {
+        const uint32_t g = (uint32_t)(L / P), p = (uint32_t)(L % P);
+        const int64_t e = G_off[L + 1];
+        for (int64_t k = G_off[L] + lane; k < e; k += 64) {
+            const uint32_t t = (uint32_t)G_tet[k];
+            keys[k] = t * (uint32_t)P + p;
+            recs[k] = make_uint2(p, g);
+            atomicAdd(&lc[t], 1u);
+        }
+    }
+}
+
+// u16 protein ids of F (k_blk's run detection reads 8 per 16-B load)
+__global__ void k_fp16(const int32_t* __restrict__ Fp, int64_t n, uint16_t* __restrict__ Fp16) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        Fp16[i] = (uint16_t)Fp[i];
+}
+
+// Both F and G given: every G entry (genome g, protein p, tetramer t) must
+// be a member of F's run (t, p) -- binary search for (p, g) in F's
+// tetramer block, which is sorted by (protein, genome).  With |G| == |F|
+// and strictly ascending lists (host-checked) G and F then hold the same
+// memberships.  One wave per list.
+__global__ __launch_bounds__(256) void k_g_check(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
+                                                 const int32_t* __restrict__ Fg, const int64_t* __restrict__ G_off,
+                                                 const int32_t* __restrict__ G_tet, int64_t n_lists, int32_t P,
+                                                 int* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t L = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); L < n_lists; L += waves) {
+        const int32_t g = (int32_t)(L / P), p = (int32_t)(L % P);
+        const uint64_t key = ((uint64_t)(uint32_t)p << 32) | (uint32_t)g;
+        const int64_t e = G_off[L + 1];
+        bool bad = false;
+        for (int64_t k = G_off[L] + lane; k < e; k += 64) {
+            const int32_t t = G_tet[k];
+            int64_t lo = Lp[t], hi = Lp[t + 1];
+            const int64_t end = hi;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                const uint64_t m = ((uint64_t)(uint32_t)Fp[mid] << 32) | (uint32_t)Fg[mid];
+                if (m < key) lo = mid + 1; else hi = mid;
+            }
+            bad |= lo >= end || Fp[lo] != p || Fg[lo] != g;
+        }
+        if (bad) atomicOr(err, 1);
+    }
+}
+
+}  // namespace pfaai

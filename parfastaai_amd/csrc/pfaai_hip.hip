@@ -13,13 +13,26 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <system_error>
 #include <vector>
 
 #include "pfaai_hip.h"
+#include "pfaai_build.hpp"
 #include "pfaai_kernels.hpp"
 #include "pfaai_rows_pl.hpp"
 
 using namespace pfaai;
+
+// Diagnostic switches that change results or instrument the kernels
+// (PFAAI_ABLATE, PFAAI_BLK_ABLATE: skip kernel phases; PFAAI_PL_CLK: stage
+// clocks; PFAAI_DIV_NEWTON: the division self-test's refinement count) exist
+// only in a library built with -DPFAAI_DIAGNOSTICS (tools/build_native.py
+// --diag -> libpfaai_hip_diag.so).  The release library never reads them.
+#ifdef PFAAI_DIAGNOSTICS
+#define DIAG_ENV(name) getenv(name)
+#else
+#define DIAG_ENV(name) (static_cast<const char*>(nullptr))
+#endif
 
 namespace {
 
@@ -115,8 +128,8 @@ int fail(pfaai_ctx* c, int code, const std::string& msg) {
 
 int hip_fail(pfaai_ctx* c, hipError_t e, const char* what) {
     if (e == hipErrorOutOfMemory)
-        return fail(c, PFAAI_ERR_OOM, std::string(what) + ": " + hipGetErrorString(e));
-    return fail(c, PFAAI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+        return fail(c, PFAAI_RC_OOM, std::string(what) + ": " + hipGetErrorString(e));
+    return fail(c, PFAAI_RC_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
 #define HIPCHK(ctx, call)                                  \
@@ -126,7 +139,7 @@ int hip_fail(pfaai_ctx* c, hipError_t e, const char* what) {
     } while (0)
 
 int ensure(pfaai_ctx* c, DevBuf& b, size_t bytes) {
-    if (b.bytes >= bytes && b.p) return PFAAI_OK;
+    if (b.bytes >= bytes && b.p) return PFAAI_RC_OK;
     if (b.p) {
         (void)hipFree(b.p);
         b.p = nullptr;
@@ -136,7 +149,7 @@ int ensure(pfaai_ctx* c, DevBuf& b, size_t bytes) {
     hipError_t e = hipMalloc(&b.p, bytes);
     if (e != hipSuccess) return hip_fail(c, e, "hipMalloc");
     b.bytes = bytes;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 void release(DevBuf& b) {
@@ -150,13 +163,14 @@ int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
     int rc = ensure(c, b, n * sizeof(T));
     if (rc) return rc;
     if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Host-side checks of pfaai_load over |F|-sized arrays: [0, n) split over up
 // to 16 threads, one per 2^20 units of `work` (default n): fn(lo, hi, thread).
+// If a thread cannot be started, its ranges run on the calling thread.
 template <class Fn>
 int par_for(int64_t n, Fn fn, int64_t work = -1) {
     const int64_t hw = std::max<int64_t>(1, (int64_t)std::thread::hardware_concurrency());
@@ -166,13 +180,78 @@ int par_for(int64_t n, Fn fn, int64_t work = -1) {
         return 1;
     }
     std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt, t); });
+    int started = 0;
+    try {
+        for (; started < nt; ++started) th.emplace_back([&, t = started] { fn(n * t / nt, n * (t + 1) / nt, t); });
+    } catch (const std::system_error&) {
+        for (int t = started; t < nt; ++t) fn(n * t / nt, n * (t + 1) / nt, t);
+    }
     for (auto& x : th) x.join();
     return nt;
 }
 
 // exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
+
+// Sort space for n keys: two key and two value ping-pong buffers, the
+// per-tile digit histograms and their scan (k_rs_hist / k_rs_scatter).
+int ensure_sort_space(pfaai_ctx* c, int64_t n) {
+    const int64_t nn = std::max<int64_t>(n, 1);
+    const int64_t ntiles = ceil_div(nn, kRsTile), hist_n = kRsBins * ntiles;
+    int rc;
+    if ((rc = ensure(c, c->key_a, nn * 4)) || (rc = ensure(c, c->key_b, nn * 4)) || (rc = ensure(c, c->val_a, nn * 4)) ||
+        (rc = ensure(c, c->val_b, nn * 4)) || (rc = ensure(c, c->hist, hist_n * 4)) ||
+        (rc = ensure(c, c->hoff, (hist_n + 1) * 8)) ||
+        (rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max<int64_t>(hist_n, PFAAI_NTETRAMERS), kScanTile)) * 8)))
+        return rc;
+    return PFAAI_RC_OK;
+}
+
+// Stable LSD radix sort (8-bit digits) of n keys with `bits` significant
+// bits; keys_in is not overwritten.  The last pass writes rec_in[original
+// index] to recs_out in key order; *sorted receives the sorted keys (one of
+// key_a / key_b).  Used for the work lists, and for F <-> G at load.
+int radix_sort_recs(pfaai_ctx* c, const uint32_t* keys_in, int64_t n, int bits, const uint2* rec_in, uint2* recs_out,
+                    hipStream_t s, const uint32_t** sorted) {
+    const int passes = std::max(1, (bits + 7) / 8);
+    const int64_t ntiles = ceil_div(std::max<int64_t>(n, 1), kRsTile);
+    auto* hist = static_cast<uint32_t*>(c->hist.p);
+    auto* hoff = static_cast<unsigned long long*>(c->hoff.p);
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = nullptr;
+    uint32_t* kout = static_cast<uint32_t*>(c->key_a.p);
+    uint32_t* vout = static_cast<uint32_t*>(c->val_a.p);
+    uint32_t* kalt = static_cast<uint32_t*>(c->key_b.p);
+    uint32_t* valt = static_cast<uint32_t*>(c->val_b.p);
+    for (int pass = 0; pass < passes; ++pass) {
+        const int shift = 8 * pass;
+        const bool first = pass == 0, last = pass == passes - 1;
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kRsThreads), 0, s, kin, n, shift, hist, ntiles);
+        int rc = scan_u32(c, hist, kRsBins * ntiles, hoff, s);
+        if (rc) return rc;
+#define RS(F, L)                                                                                                  \
+    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, hist, \
+                       ntiles, kout, vout, rec_in, recs_out)
+        if (first && last) RS(true, true);
+        else if (first) RS(true, false);
+        else if (last) RS(false, true);
+        else RS(false, false);
+#undef RS
+        kin = kout;  // ping-pong (never back into keys_in)
+        vin = vout;
+        std::swap(kout, kalt);
+        std::swap(vout, valt);
+    }
+    if (sorted) *sorted = kin;
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_RC_OK;
+}
+
+int bits_for(int64_t k) {  // significant bits of keys < k
+    int bits = 1;
+    while (bits < 32 && ((int64_t)1 << bits) < k) ++bits;
+    return bits;
+}
 
 // Work-list build for rows [rb, re): entries, LSD radix sort, rowptr.
 template <int MODE>
@@ -201,45 +280,14 @@ int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool firs
     if (n == 0) {
         HIPCHK(c, hipMemsetAsync(rowptr, 0, (K + 1) * sizeof(unsigned long long), s));
         HIPCHK(c, hipGetLastError());
-        return PFAAI_OK;
+        return PFAAI_RC_OK;
     }
-    int bits = 1;
-    while (bits < 32 && ((int64_t)1 << bits) < K) ++bits;
-    const int passes = (bits + 7) / 8;
-    const int64_t ntiles = ceil_div(n, kRsTile);
-    auto* hist = static_cast<uint32_t*>(c->hist.p);
-    auto* hoff = static_cast<unsigned long long*>(c->hoff.p);
-    uint32_t* kin = key_c;
-    uint32_t* vin = nullptr;
-    uint32_t* kout = static_cast<uint32_t*>(c->key_a.p);
-    uint32_t* vout = static_cast<uint32_t*>(c->val_a.p);
-    uint32_t* kalt = static_cast<uint32_t*>(c->key_b.p);
-    uint32_t* valt = static_cast<uint32_t*>(c->val_b.p);
-    auto* recs = static_cast<uint2*>(c->recs.p);
-    for (int pass = 0; pass < passes; ++pass) {
-        const int shift = 8 * pass;
-        const bool first = pass == 0, last = pass == passes - 1;
-        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kRsThreads), 0, s, kin, n, shift, hist, ntiles);
-        int rc = scan_u32(c, hist, kRsBins * ntiles, hoff, s);
-        if (rc) return rc;
-#define RS(F, L)                                                                                                  \
-    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, hist, \
-                       ntiles, kout, vout, rec_c, recs)
-        if (first && last) RS(true, true);
-        else if (first) RS(true, false);
-        else if (last) RS(false, true);
-        else RS(false, false);
-#undef RS
-        // ping-pong (never back into key_c, the entries' own buffer)
-        kin = kout;
-        vin = vout;
-        std::swap(kout, kalt);
-        std::swap(vout, valt);
-    }
-    const uint32_t* ksorted = kin;
+    const uint32_t* ksorted = nullptr;
+    int rc = radix_sort_recs(c, key_c, n, bits_for(K), rec_c, static_cast<uint2*>(c->recs.p), s, &ksorted);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_rowptr, dim3(ceil_div(n, 256)), dim3(256), 0, s, ksorted, n, K, rowptr);
     HIPCHK(c, hipGetLastError());
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 // Fused genome-major path: only the run table (+ the first E triple for the
@@ -249,7 +297,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
-    const int dbg = getenv("PFAAI_BLK_ABLATE") ? atoi(getenv("PFAAI_BLK_ABLATE")) : 0;
+    const int dbg = DIAG_ENV("PFAAI_BLK_ABLATE") ? atoi(DIAG_ENV("PFAAI_BLK_ABLATE")) : 0;
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
     // 1024 threads (0.649 vs 0.666 ms at 10k; the window form gains 2x, see
     // run_mode); PFAAI_BLK_THREADS=256 for A/B
@@ -267,7 +315,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
                            static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
     }
     HIPCHK(c, hipGetLastError());
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s) {
@@ -278,7 +326,7 @@ int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* ou
     hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, s, sums, tiles, sc + SC_GRAND);
     hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(kScanThreads), 0, s, out, n, sums, sc + SC_GRAND,
                        static_cast<unsigned long long*>(nullptr));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 // Counter words per thread: the smallest KW with KW * nt >= the widest row
@@ -361,7 +409,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     if (c->rows_kernel == RK_PL) {
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
-        if (MODE == 0 && kw == 5 && !c->windows && getenv("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+#ifdef PFAAI_DIAGNOSTICS
+        if (MODE == 0 && kw == 5 && !c->windows && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
             const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
             const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
@@ -371,6 +420,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
                                static_cast<unsigned long long*>(c->dbg.p));
             return;
         }
+#endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
         const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
         if (nl) {
@@ -413,7 +463,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
 // it is allocated at load only for F-only input (and on first use by
 // pfaai_debug_row_counts).
 int ensure_worklists(pfaai_ctx* c) {
-    if (c->wl_ready) return PFAAI_OK;
+    if (c->wl_ready) return PFAAI_RC_OK;
     const auto& p = c->prob;
     int rc;
     const int64_t nmax = std::max<int64_t>(1, c->row_fprefix[c->n_rows]);
@@ -437,7 +487,7 @@ int ensure_worklists(pfaai_ctx* c) {
                                      sizeof(unsigned long long))))
         return rc;
     c->wl_ready = true;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 template <int MODE>
@@ -460,11 +510,11 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
             nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
             win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * (int64_t)c->prob.n_prot * nwin));
             c->windows = win_tile >= 1 &&
-                         ensure(c, c->blkw, (size_t)nwin * c->prob.n_prot * kNTetramers * sizeof(uint4)) == PFAAI_OK;
+                         ensure(c, c->blkw, (size_t)nwin * c->prob.n_prot * kNTetramers * sizeof(uint4)) == PFAAI_RC_OK;
         }
     }
     if (c->windows) {
-        if (!c->take_events()) return fail(c, PFAAI_ERR_HIP, "hipEventCreate failed");
+        if (!c->take_events()) return fail(c, PFAAI_RC_HIP, "hipEventCreate failed");
         HIPCHK(c, hipEventRecord(c->ev0, s));
         // the window tables depend only on the loaded F and the window width
         const bool keep = (flags & PFAAI_FLAG_KEEP_RUNS) && c->win_valid && c->win_cols == wcols &&
@@ -500,10 +550,10 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(c->ev2, s));
-        return PFAAI_OK;
+        return PFAAI_RC_OK;
     }
     // three events per run: start, after work-list build, after row kernel
-    if (!c->take_events()) return fail(c, PFAAI_ERR_HIP, "hipEventCreate failed");
+    if (!c->take_events()) return fail(c, PFAAI_RC_HIP, "hipEventCreate failed");
     HIPCHK(c, hipEventRecord(c->ev0, s));
     if (wl) {
         const int rcw = ensure_worklists(c);
@@ -513,11 +563,11 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     // run over further rows of the same problem may reuse it (stream-ordered
     // after the run that built it)
     const bool keep = !wl && (flags & PFAAI_FLAG_KEEP_RUNS) && c->runs_valid && (c->runs_key || !compat);
-    int rc = PFAAI_OK;
+    int rc = PFAAI_RC_OK;
     if (wl) rc = build_records<MODE>(c, rb, re, s, compat);
     else if (!keep) {
         rc = build_runs_g<MODE>(c, s, compat);
-        c->runs_valid = rc == PFAAI_OK;
+        c->runs_valid = rc == PFAAI_RC_OK;
         c->runs_key = compat;
     }
     if (rc) return rc;
@@ -525,93 +575,223 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     launch_rows<MODE>(c, rb, re, flags, aji, S, N, s);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev2, s));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int pfaai_version(void) { return PFAAI_ABI_VERSION; }
-
-int pfaai_create(pfaai_ctx** out, int device_id) {
-    if (!out) return PFAAI_ERR_INVALID;
-    *out = nullptr;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PFAAI_ERR_HIP;
-    if (device_id < 0 || device_id >= ndev) return PFAAI_ERR_INVALID;
-    auto* c = new pfaai_ctx();
-    c->device = device_id;
-    if (hipSetDevice(device_id) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return PFAAI_ERR_HIP;
+// Run fn() and map a C++ exception to an error code: nothing may unwind
+// through the C ABI (a std::bad_alloc of a host vector, a std::system_error
+// of a checking thread).
+template <class Fn>
+int guarded(pfaai_ctx* c, Fn fn) {
+    try {
+        return fn();
+    } catch (const std::bad_alloc&) {
+        return fail(c, PFAAI_RC_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(c, PFAAI_RC_INVALID, std::string("internal error: ") + e.what());
+    } catch (...) {
+        return fail(c, PFAAI_RC_INVALID, "internal error");
     }
-    int rc = ensure(c, c->scalars, SC_N * sizeof(unsigned long long));
-    if (rc) {
-        delete c;
+}
+
+// F from G on the device (the CLI's `<p>_genomes` read; F never exists on
+// the host): keys t * P + p, stable radix sort, split into Fp / Fg, Lp by a
+// scan of the tetramer counts.
+int build_f_from_g(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
+    const int32_t P = c->prob.n_prot;
+    int rc;
+    if ((rc = ensure(c, c->key_c, std::max<int64_t>(n, 1) * 4)) || (rc = ensure(c, c->rec_c, std::max<int64_t>(n, 1) * 8)) ||
+        (rc = ensure(c, c->recs, std::max<int64_t>(n, 1) * 8)) || (rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * 4)) ||
+        (rc = ensure_sort_space(c, n)))
         return rc;
+    auto* lc = static_cast<uint32_t*>(c->cnt_t.p);
+    HIPCHK(c, hipMemsetAsync(lc, 0, PFAAI_NTETRAMERS * 4, s));
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n_lists, 4), 1), 1 << 16);
+    hipLaunchKernelGGL(k_fkeys_from_g, dim3(grid), dim3(256), 0, s, static_cast<const int64_t*>(c->G_off.p),
+                       static_cast<const int32_t*>(c->G_tet.p), n_lists, P, static_cast<uint32_t*>(c->key_c.p),
+                       static_cast<uint2*>(c->rec_c.p), lc);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = scan_u32(c, lc, PFAAI_NTETRAMERS, static_cast<unsigned long long*>(c->Lp.p), s))) return rc;
+    if (n) {
+        auto* recs = static_cast<uint2*>(c->recs.p);
+        if ((rc = radix_sort_recs(c, static_cast<const uint32_t*>(c->key_c.p), n, bits_for((int64_t)PFAAI_NTETRAMERS * P),
+                                  static_cast<const uint2*>(c->rec_c.p), recs, s, nullptr)))
+            return rc;
+        const int g2 = (int)std::min<int64_t>(ceil_div(n, 256), 1 << 16);
+        hipLaunchKernelGGL(k_f_split, dim3(g2), dim3(256), 0, s, recs, n, static_cast<int32_t*>(c->Fp.p),
+                           static_cast<int32_t*>(c->Fg.p));
+        HIPCHK(c, hipGetLastError());
     }
-    (void)hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long));
-    *out = c;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
-int pfaai_destroy(pfaai_ctx* c) {
-    if (!c) return PFAAI_OK;
-    (void)hipSetDevice(c->device);
-    (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
-                      &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
-                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw})
+// G from F on the device (F-only callers, e.g. the reference's own
+// DataStructInterface classes): keys g * P + p, stable radix sort, G_tet from
+// the sorted (tetramer, genome) records, G_off = first sorted key >= k.
+int build_g_from_f(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
+    const int32_t P = c->prob.n_prot;
+    int rc;
+    if ((rc = ensure(c, c->key_c, std::max<int64_t>(n, 1) * 4)) || (rc = ensure(c, c->rec_c, std::max<int64_t>(n, 1) * 8)) ||
+        (rc = ensure(c, c->recs, std::max<int64_t>(n, 1) * 8)) || (rc = ensure_sort_space(c, n)) ||
+        (rc = ensure(c, c->G_off, (n_lists + 1) * 8)) || (rc = ensure(c, c->G_tet, std::max<int64_t>(n, 1) * 4)))
+        return rc;
+    auto* goff = static_cast<unsigned long long*>(c->G_off.p);
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(goff, 0, (n_lists + 1) * 8, s));
+        return PFAAI_RC_OK;
+    }
+    hipLaunchKernelGGL(k_gkeys_from_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
+                       static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), P,
+                       static_cast<uint32_t*>(c->key_c.p), static_cast<uint2*>(c->rec_c.p));
+    HIPCHK(c, hipGetLastError());
+    auto* recs = static_cast<uint2*>(c->recs.p);
+    const uint32_t* ksorted = nullptr;
+    if ((rc = radix_sort_recs(c, static_cast<const uint32_t*>(c->key_c.p), n, bits_for(n_lists),
+                              static_cast<const uint2*>(c->rec_c.p), recs, s, &ksorted)))
+        return rc;
+    const int g2 = (int)std::min<int64_t>(ceil_div(n, 256), 1 << 16);
+    hipLaunchKernelGGL(k_gtet_split, dim3(g2), dim3(256), 0, s, recs, n, static_cast<int32_t*>(c->G_tet.p));
+    hipLaunchKernelGGL(k_rowptr, dim3(ceil_div(n, 256)), dim3(256), 0, s, ksorted, n, n_lists, goff);
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_RC_OK;
+}
+
+// The load-time sort space is also the work-list space: release it when the
+// genome-major kernels (which need none of it) will run.
+void release_sort_space(pfaai_ctx* c) {
+    for (DevBuf* b : {&c->key_c, &c->rec_c, &c->recs, &c->key_a, &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff})
         release(*b);
-    for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
-    release(c->st_dev);
-    if (c->st_host) (void)hipHostFree(c->st_host);
-    for (int i = 0; i < 2; ++i) {
-        if (c->st_done[i]) (void)hipEventDestroy(c->st_done[i]);
-        if (c->st_copied[i]) (void)hipEventDestroy(c->st_copied[i]);
-    }
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    delete c;
-    return PFAAI_OK;
+    c->wl_ready = false;
 }
 
-const char* pfaai_last_error(const pfaai_ctx* c) { return c ? c->err.c_str() : "null context"; }
-
-int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
-    if (!c || !pb) return PFAAI_ERR_INVALID;
+int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     HIPCHK(c, hipSetDevice(c->device));
     c->loaded = false;
     const pfaai_problem& p = *pb;
-    if (p.mode < 0 || p.mode > 2) return fail(c, PFAAI_ERR_INVALID, "mode must be 0, 1 or 2");
+    if (p.mode < 0 || p.mode > 2) return fail(c, PFAAI_RC_INVALID, "mode must be 0, 1 or 2");
     if (p.n_ids < 2 || p.n_prot < 1 || p.n_prot >= kMaxRuns || p.t_cols < 1)
-        return fail(c, PFAAI_ERR_INVALID, "bad sizes (n_ids >= 2, 1 <= n_prot < 4096)");
+        return fail(c, PFAAI_RC_INVALID, "bad sizes (n_ids >= 2, 1 <= n_prot < 4096)");
     // 21-bit genome ids (run-table splitters, first-key packing); F indices
     // are u32 in the run table / work lists (and 16-B records in k_rows_pl)
-    if (p.n_ids >= (1 << 21) || p.n_f < 0 || p.n_f > kMaxF)
-        return fail(c, PFAAI_ERR_INVALID, "n_ids must be < 2^21 and |F| <= 2^32 - 64");
-    if (!p.Lp || !p.F_prot || !p.F_genome || !p.T)
-        return fail(c, PFAAI_ERR_INVALID, "Lp, F_prot, F_genome and T are required");
-    if (p.Lp[0] != 0 || p.Lp[PFAAI_NTETRAMERS] != p.n_f)
-        return fail(c, PFAAI_ERR_INVALID, "Lp must start at 0 and end at n_f");
-    if (p.mode != PFAAI_MODE_ALL && !p.is_q)
-        return fail(c, PFAAI_ERR_INVALID, "is_q is required for QSUB/QT");
+    if (p.n_ids >= (1 << 21)) return fail(c, PFAAI_RC_INVALID, "n_ids must be < 2^21");
+    const bool in_f = p.Lp || p.F_prot || p.F_genome;
+    const bool in_g = p.G_off || p.G_tet;
+    if (in_f && !(p.Lp && p.F_prot && p.F_genome))
+        return fail(c, PFAAI_RC_INVALID, "Lp, F_prot and F_genome are required together");
+    if (in_g && !(p.G_off && p.G_tet)) return fail(c, PFAAI_RC_INVALID, "G_off and G_tet are required together");
+    if (!in_f && !in_g) return fail(c, PFAAI_RC_INVALID, "F (Lp, F_prot, F_genome) or G (G_off, G_tet) is required");
+    if (!p.T) return fail(c, PFAAI_RC_INVALID, "T is required");
+    if (p.mode != PFAAI_MODE_ALL && !p.is_q) return fail(c, PFAAI_RC_INVALID, "is_q is required for QSUB/QT");
     if (p.mode == PFAAI_MODE_QSUB && (!p.q_index || !p.t_rank))
-        return fail(c, PFAAI_ERR_INVALID, "q_index and t_rank are required for QSUB");
+        return fail(c, PFAAI_RC_INVALID, "q_index and t_rank are required for QSUB");
     if (p.mode == PFAAI_MODE_QT && p.n_ids != p.n_tgt + p.n_qry)
-        return fail(c, PFAAI_ERR_INVALID, "QT: n_ids must equal n_tgt + n_qry");
+        return fail(c, PFAAI_RC_INVALID, "QT: n_ids must equal n_tgt + n_qry");
+    if (p.t_cols < p.n_ids) return fail(c, PFAAI_RC_INVALID, "T needs a column per genome id");
+    const int32_t ni = p.n_ids, P = p.n_prot;
     // T must hold every count < 2^16 (packed u16 LDS counters; c <= min T)
-    const int64_t tn = (int64_t)p.n_prot * p.t_cols;
-    for (int64_t i = 0; i < tn; ++i)
-        if (p.T[i] < 0 || p.T[i] > 65535) return fail(c, PFAAI_ERR_INVALID, "T entries must lie in [0, 65535]");
+    const int64_t tn = (int64_t)P * p.t_cols;
+    {
+        std::atomic<int> bad{0};
+        par_for(tn, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t i = lo; i < hi; ++i)
+                if (p.T[i] < 0 || p.T[i] > 65535) { bad = 1; return; }
+        });
+        if (bad) return fail(c, PFAAI_RC_INVALID, "T entries must lie in [0, 65535]");
+    }
+
+    // G: offsets first (they bound every G_tet access), then the entries:
+    // tetramer ids in range, each (genome, protein) list strictly ascending
+    const int64_t ng = (int64_t)ni * P;
+    int64_t n_g = 0;
+    c->max_glen = 0;
+    if (in_g) {
+        if (p.G_off[0] != 0) return fail(c, PFAAI_RC_INVALID, "G_off must start at 0");
+        std::atomic<int> bad_off{0};
+        par_for(ng, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k)
+                if (p.G_off[k + 1] < p.G_off[k]) { bad_off = 1; return; }
+        });
+        if (bad_off) return fail(c, PFAAI_RC_INVALID, "G_off must be non-decreasing");
+        n_g = p.G_off[ng];
+        if (n_g > kMaxF) return fail(c, PFAAI_RC_INVALID, "|G| must be <= 2^32 - 64");
+        std::atomic<int> bad_t{0}, bad_ord{0};
+        std::vector<int64_t> mx(16, 0);
+        par_for(
+            ng,
+            [&](int64_t lo, int64_t hi, int th) {
+                int64_t m = 0;
+                for (int64_t k = lo; k < hi; ++k) {
+                    const int64_t b = p.G_off[k], e = p.G_off[k + 1];
+                    m = std::max(m, e - b);
+                    for (int64_t i = b; i < e; ++i) {
+                        if (p.G_tet[i] < 0 || p.G_tet[i] >= PFAAI_NTETRAMERS) { bad_t = 1; return; }
+                        if (i > b && p.G_tet[i] <= p.G_tet[i - 1]) { bad_ord = 1; return; }
+                    }
+                }
+                mx[th] = m;
+            },
+            n_g);
+        if (bad_t) return fail(c, PFAAI_RC_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
+        if (bad_ord) return fail(c, PFAAI_RC_INVALID, "every G list must be strictly ascending");
+        for (int64_t m : mx) c->max_glen = std::max(c->max_glen, m);
+    }
+
+    // F: Lp first (it bounds every F access): starts at 0, ends at n_f,
+    // non-decreasing; then ids in range and the (tetramer, protein, genome)
+    // order of ds_helper.hpp:126-162 that the run table relies on
+    const int64_t n_f = in_f ? p.n_f : n_g;
+    if (n_f < 0 || n_f > kMaxF) return fail(c, PFAAI_RC_INVALID, "|F| must be <= 2^32 - 64");
+    std::vector<int64_t> fcount(ni, 0);  // F entries per genome (work-list sizes)
+    if (in_f) {
+        if (p.Lp[0] != 0 || p.Lp[PFAAI_NTETRAMERS] != p.n_f)
+            return fail(c, PFAAI_RC_INVALID, "Lp must start at 0 and end at n_f");
+        for (int t = 0; t < PFAAI_NTETRAMERS; ++t)
+            if (p.Lp[t + 1] < p.Lp[t]) return fail(c, PFAAI_RC_INVALID, "Lp must be non-decreasing");
+        if (in_g && n_g != n_f) return fail(c, PFAAI_RC_INVALID, "G must list exactly F's memberships (|G| != |F|)");
+        std::vector<std::vector<int64_t>> fc(16);
+        std::atomic<int> bad_id{0}, bad_p{0}, bad_sort{0};
+        const int nth = par_for(p.n_f, [&](int64_t lo, int64_t hi, int t) {
+            std::vector<int64_t>& cnt = fc[t];
+            cnt.assign(ni, 0);
+            for (int64_t i = lo; i < hi; ++i) {
+                const int32_t g = p.F_genome[i];
+                if (g < 0 || g >= ni) { bad_id = 1; return; }
+                if (p.F_prot[i] < 0 || p.F_prot[i] >= P) { bad_p = 1; return; }
+                cnt[g]++;
+            }
+        });
+        if (bad_id) return fail(c, PFAAI_RC_INVALID, "F holds a genome id outside [0, n_ids)");
+        if (bad_p) return fail(c, PFAAI_RC_INVALID, "F holds a protein id outside [0, n_prot)");
+        for (int t = 0; t < nth; ++t)
+            for (int32_t g = 0; g < ni; ++g) fcount[g] += fc[t][g];
+        par_for(
+            PFAAI_NTETRAMERS,
+            [&](int64_t lo, int64_t hi, int) {
+                for (int64_t t = lo; t < hi; ++t)
+                    for (int64_t i = p.Lp[t] + 1; i < p.Lp[t + 1]; ++i)
+                        if (p.F_prot[i] < p.F_prot[i - 1] ||
+                            (p.F_prot[i] == p.F_prot[i - 1] && p.F_genome[i] <= p.F_genome[i - 1])) {
+                            bad_sort = 1;
+                            return;
+                        }
+            },
+            p.n_f);
+        if (bad_sort) return fail(c, PFAAI_RC_INVALID, "F must be sorted by (tetramer, protein, genome)");
+    } else {
+        for (int32_t g = 0; g < ni; ++g) fcount[g] = p.G_off[(int64_t)(g + 1) * P] - p.G_off[(int64_t)g * P];
+    }
 
     c->prob = p;
+    c->prob.n_f = n_f;
+    // borrowed host arrays are not kept past this call
+    c->prob.Lp = nullptr;
+    c->prob.F_prot = c->prob.F_genome = c->prob.T = nullptr;
+    c->prob.is_q = nullptr;
+    c->prob.q_index = c->prob.t_rank = nullptr;
+    c->prob.G_off = nullptr;
+    c->prob.G_tet = nullptr;
     c->runs_valid = c->runs_key = false;
     c->win_valid = c->win_key = false;
-    const int32_t ni = p.n_ids;
     // output rows and derived maps
     std::vector<int32_t> row_of(ni, -1), tcol_row(ni), tcol_col(ni);
     c->row_genome_h.clear();
@@ -629,12 +809,12 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         for (int32_t g = 0; g < ni; ++g) {
             if (!p.is_q[g]) continue;
             const int32_t qi = p.q_index[g];
-            if (qi < 0 || qi >= p.n_qry) return fail(c, PFAAI_ERR_INVALID, "q_index out of range");
+            if (qi < 0 || qi >= p.n_qry) return fail(c, PFAAI_RC_INVALID, "q_index out of range");
             row_of[g] = qi;
             c->row_genome_h[qi] = g;
         }
         for (int32_t x : c->row_genome_h)
-            if (x < 0) return fail(c, PFAAI_ERR_INVALID, "query list has holes");
+            if (x < 0) return fail(c, PFAAI_RC_INVALID, "query list has holes");
         c->n_rows = p.n_qry;
         c->n_pairs = (int64_t)p.n_qry * p.n_tgt + (int64_t)p.n_qry * (p.n_qry - 1) / 2;
         c->max_cols = ni;
@@ -661,14 +841,9 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
                 tcol_col[g] = std::min(tcol_col[g], p.t_cols - 1);
             }
     }
-    for (int32_t g = 0; g < ni; ++g)
-        if (g >= p.t_cols) return fail(c, PFAAI_ERR_INVALID, "T needs a column per genome id");
 
     int rc;
-    if ((rc = upload(c, c->Lp, p.Lp, PFAAI_NTETRAMERS + 1))) return rc;
-    if ((rc = upload(c, c->Fp, p.F_prot, p.n_f))) return rc;
-    if ((rc = ensure(c, c->Fg, (p.n_f + 16) * sizeof(int32_t)))) return rc;  // int4 reads may pass the end
-    if ((rc = upload(c, c->Fg, p.F_genome, p.n_f))) return rc;
+    hipStream_t s = c->stream;
     if ((rc = upload(c, c->T, p.T, tn))) return rc;
     std::vector<uint8_t> isq(ni, 1);
     if (p.is_q) isq.assign(p.is_q, p.is_q + ni);
@@ -688,12 +863,12 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     c->dev.t16_cols = ((int64_t)ni + 15) & ~(int64_t)7;  // 16-B rows, >= n_ids + 8 (uint4 reads past chi)
     {
         const int64_t tc = c->dev.t16_cols;
-        std::vector<uint16_t> t16((size_t)p.n_prot * tc, 0);
-        for (int64_t q = 0; q < p.n_prot; ++q)
+        std::vector<uint16_t> t16((size_t)P * tc, 0);
+        for (int64_t q = 0; q < P; ++q)
             for (int32_t g = 0; g < ni; ++g) t16[q * tc + g] = (uint16_t)p.T[q * p.t_cols + g];
         if ((rc = upload(c, c->T16, t16.data(), t16.size()))) return rc;
         if (p.mode == PFAAI_MODE_QT) {
-            for (int64_t q = 0; q < p.n_prot; ++q)
+            for (int64_t q = 0; q < P; ++q)
                 for (int32_t g = 0; g < ni; ++g) t16[q * tc + g] = (uint16_t)p.T[q * p.t_cols + tcol_col[g]];
             if ((rc = upload(c, c->T16c, t16.data(), t16.size()))) return rc;
         } else {
@@ -701,41 +876,65 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
         }
     }
 
-    c->has_g = p.G_off && p.G_tet;
-    if (c->has_g) {
-        const int64_t ng = (int64_t)ni * p.n_prot;
-        if (p.G_off[0] != 0) return fail(c, PFAAI_ERR_INVALID, "G_off must start at 0");
-        for (int64_t k = 0; k < ng; ++k)
-            if (p.G_off[k + 1] < p.G_off[k]) return fail(c, PFAAI_ERR_INVALID, "G_off must be non-decreasing");
-        const int64_t gt = p.G_off[ng];
-        if (gt >= ((int64_t)1 << 32)) return fail(c, PFAAI_ERR_INVALID, "G too large");
-        std::atomic<int> bad_g{0};
-        par_for(gt, [&](int64_t lo, int64_t hi, int) {
-            for (int64_t k = lo; k < hi; ++k)
-                if (p.G_tet[k] < 0 || p.G_tet[k] >= PFAAI_NTETRAMERS) { bad_g = 1; return; }
-        });
-        if (bad_g) return fail(c, PFAAI_ERR_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
-        c->max_glen = 0;
-        for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, p.G_off[k + 1] - p.G_off[k]);
+    // F and G on the device, whichever the caller did not give built from
+    // the other (pfaai_build.hpp)
+    if ((rc = ensure(c, c->Lp, (PFAAI_NTETRAMERS + 1) * sizeof(int64_t)))) return rc;
+    if ((rc = ensure(c, c->Fp, std::max<int64_t>(n_f, 1) * sizeof(int32_t)))) return rc;
+    if ((rc = ensure(c, c->Fg, (n_f + 16) * sizeof(int32_t)))) return rc;  // int4 reads may pass the end
+    if (in_g) {
         if ((rc = upload(c, c->G_off, p.G_off, ng + 1))) return rc;
-        if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(gt, 1)))) return rc;
-        if ((rc = ensure(c, c->blk, (size_t)p.n_prot * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
-        // u16 protein ids of F for k_blk's run detection (n_prot < 4096)
-        std::vector<uint16_t> fp16((size_t)p.n_f + 16, 0);  // 16-B reads may pass the end
-        par_for(p.n_f, [&](int64_t lo, int64_t hi, int) {
-            for (int64_t i = lo; i < hi; ++i) fp16[i] = (uint16_t)p.F_prot[i];
-        });
-        if ((rc = upload(c, c->Fp16, fp16.data(), fp16.size()))) return rc;
+        if ((rc = upload(c, c->G_tet, p.G_tet, std::max<int64_t>(n_g, 1)))) return rc;
     }
+    if (in_f) {
+        if ((rc = upload(c, c->Lp, p.Lp, PFAAI_NTETRAMERS + 1))) return rc;
+        if ((rc = upload(c, c->Fp, p.F_prot, n_f))) return rc;
+        if ((rc = upload(c, c->Fg, p.F_genome, n_f))) return rc;
+    } else if ((rc = build_f_from_g(c, ng, n_f, s))) {
+        return rc;
+    }
+    bool has_g = in_g;
+    if (in_g && in_f && n_f) {  // both given: G must list F's memberships
+        auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+        int* err = reinterpret_cast<int*>(sc + SC_ERR);
+        HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_g_check, dim3((int)std::min<int64_t>(ceil_div(ng, 4), 1 << 16)), dim3(256), 0, s,
+                           static_cast<const int64_t*>(c->Lp.p), static_cast<const int32_t*>(c->Fp.p),
+                           static_cast<const int32_t*>(c->Fg.p), static_cast<const int64_t*>(c->G_off.p),
+                           static_cast<const int32_t*>(c->G_tet.p), ng, P, err);
+        HIPCHK(c, hipGetLastError());
+        int bad = 0;
+        HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (bad) return fail(c, PFAAI_RC_INVALID, "G lists a membership that F does not hold");
+    } else if (!in_g && ng < ((int64_t)1 << 32)) {  // G from F (keys g * P + p fit 32 bits)
+        if ((rc = build_g_from_f(c, ng, n_f, s))) return rc;
+        std::vector<int64_t> goff(ng + 1);
+        HIPCHK(c, hipMemcpyAsync(goff.data(), c->G_off.p, (ng + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, goff[k + 1] - goff[k]);
+        has_g = true;
+    }
+    c->has_g = has_g;
+    if (!has_g) {
+        release(c->G_off);
+        release(c->G_tet);
+    }
+    if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
+    HIPCHK(c, hipMemsetAsync(c->Fp16.p, 0, (n_f + 16) * sizeof(uint16_t), s));
+    if (n_f)
+        hipLaunchKernelGGL(k_fp16, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 1 << 16)), dim3(256), 0, s,
+                           static_cast<const int32_t*>(c->Fp.p), n_f, static_cast<uint16_t*>(c->Fp16.p));
+    HIPCHK(c, hipGetLastError());
+    if (has_g && (rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
 
     Dev& d = c->dev;
     d.mode = p.mode;
     d.n_ids = ni;
-    d.n_prot = p.n_prot;
+    d.n_prot = P;
     d.t_cols = p.t_cols;
     d.n_qry = c->prob.n_qry;
     d.n_tgt = c->prob.n_tgt;
-    d.n_f = p.n_f;
+    d.n_f = n_f;
     d.Lp = static_cast<const int64_t*>(c->Lp.p);
     d.Fp = static_cast<const int32_t*>(c->Fp.p);
     d.Fg = static_cast<const int32_t*>(c->Fg.p);
@@ -747,73 +946,91 @@ int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     d.row_genome = static_cast<const int32_t*>(c->row_genome.p);
     d.tcol_row = static_cast<const int32_t*>(c->tcol_row.p);
     d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
-    d.G_off = c->has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
-    d.G_tet = c->has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
-    d.blk = c->has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
-    d.Fp16 = c->has_g ? static_cast<const uint16_t*>(c->Fp16.p) : nullptr;
+    d.G_off = has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
+    d.G_tet = has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
+    d.blk = has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
+    d.Fp16 = static_cast<const uint16_t*>(c->Fp16.p);
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
     d.T16c = c->T16c.p ? static_cast<const uint16_t*>(c->T16c.p) : d.T16;
 
-    // Work space sized for all rows, so pfaai_run never allocates or syncs.
-    // Work-list entries of a row = F entries of its genome (counted here).
-    {
-        std::vector<int64_t> fcount(ni, 0);
-        std::vector<std::vector<int64_t>> fc(16);
-        std::atomic<int> bad_id{0}, bad_p{0}, bad_sort{0};
-        const int nth = par_for(p.n_f, [&](int64_t lo, int64_t hi, int t) {
-            std::vector<int64_t>& cnt = fc[t];
-            cnt.assign(ni, 0);
-            for (int64_t i = lo; i < hi; ++i) {
-                const int32_t g = p.F_genome[i];
-                if (g < 0 || g >= ni) { bad_id = 1; return; }
-                if (p.F_prot[i] < 0 || p.F_prot[i] >= p.n_prot) { bad_p = 1; return; }
-                cnt[g]++;
-            }
-        });
-        if (bad_id) return fail(c, PFAAI_ERR_INVALID, "F holds a genome id outside [0, n_ids)");
-        if (bad_p) return fail(c, PFAAI_ERR_INVALID, "F holds a protein id outside [0, n_prot)");
-        for (int t = 0; t < nth; ++t)
-            for (int32_t g = 0; g < ni; ++g) fcount[g] += fc[t][g];
-        // F sorted by (tetramer, protein, genome) -- ds_helper.hpp:126-162; the
-        // run table and the line pruning rely on it (checked by tetramer blocks)
-        par_for(
-            PFAAI_NTETRAMERS,
-            [&](int64_t lo, int64_t hi, int) {
-                for (int64_t t = lo; t < hi; ++t)
-                    for (int64_t i = p.Lp[t] + 1; i < p.Lp[t + 1]; ++i)
-                        if (p.F_prot[i] < p.F_prot[i - 1] ||
-                            (p.F_prot[i] == p.F_prot[i - 1] && p.F_genome[i] <= p.F_genome[i - 1])) {
-                            bad_sort = 1;
-                            return;
-                        }
-            },
-            p.n_f);
-        if (bad_sort) return fail(c, PFAAI_ERR_INVALID, "F must be sorted by (tetramer, protein, genome)");
-        c->row_fprefix.assign(c->n_rows + 1, 0);
-        for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
-        if (c->has_g) {  // work lists follow G (one record per G entry of a row genome)
-            for (int64_t r = 0; r < c->n_rows; ++r) {
-                const int64_t g0 = (int64_t)c->row_genome_h[r] * p.n_prot;
-                c->row_fprefix[r + 1] = c->row_fprefix[r] + (p.G_off[g0 + p.n_prot] - p.G_off[g0]);
-            }
-        }
-    }
-    HIPCHK(c, hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long)));
-    c->wl_ready = false;
-    if (!c->has_g && (rc = ensure_worklists(c))) return rc;
+    // work-list sizes (exact: one record per F entry of a row genome)
+    c->row_fprefix.assign(c->n_rows + 1, 0);
+    for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
+    HIPCHK(c, hipMemsetAsync(c->scalars.p, 0, SC_N * sizeof(unsigned long long), s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    release_sort_space(c);  // pfaai_run never allocates; the work-list path re-allocates below
+    if (!has_g && (rc = ensure_worklists(c))) return rc;
     c->loaded = true;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfaai_version(void) { return PFAAI_ABI_VERSION; }
+
+int pfaai_create(pfaai_ctx** out, int device_id) {
+    if (!out) return PFAAI_RC_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PFAAI_RC_HIP;
+    if (device_id < 0 || device_id >= ndev) return PFAAI_RC_INVALID;
+    auto* c = new pfaai_ctx();
+    c->device = device_id;
+    if (hipSetDevice(device_id) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PFAAI_RC_HIP;
+    }
+    int rc = ensure(c, c->scalars, SC_N * sizeof(unsigned long long));
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    (void)hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long));
+    *out = c;
+    return PFAAI_RC_OK;
+}
+
+int pfaai_destroy(pfaai_ctx* c) {
+    if (!c) return PFAAI_RC_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
+                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw})
+        release(*b);
+    for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
+    release(c->st_dev);
+    if (c->st_host) (void)hipHostFree(c->st_host);
+    for (int i = 0; i < 2; ++i) {
+        if (c->st_done[i]) (void)hipEventDestroy(c->st_done[i]);
+        if (c->st_copied[i]) (void)hipEventDestroy(c->st_copied[i]);
+    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return PFAAI_RC_OK;
+}
+
+const char* pfaai_last_error(const pfaai_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
+    if (!c || !pb) return PFAAI_RC_INVALID;
+    return guarded(c, [&] { return load_impl(c, pb); });
 }
 
 int pfaai_shape(const pfaai_ctx* c, int64_t* n_rows, int64_t* n_pairs) {
-    if (!c || !c->loaded) return PFAAI_ERR_INVALID;
+    if (!c || !c->loaded) return PFAAI_RC_INVALID;
     if (n_rows) *n_rows = c->n_rows;
     if (n_pairs) *n_pairs = c->n_pairs;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_row_span(const pfaai_ctx* c, int64_t rb, int64_t re, int64_t* first, int64_t* count) {
-    if (!c || !c->loaded || rb < 0 || re > c->n_rows || rb > re) return PFAAI_ERR_INVALID;
+    if (!c || !c->loaded || rb < 0 || re > c->n_rows || rb > re) return PFAAI_RC_INVALID;
     const auto& p = c->prob;
     int64_t f = 0, l = 0;  // [f, l)
     if (rb == re) {
@@ -833,16 +1050,16 @@ int pfaai_row_span(const pfaai_ctx* c, int64_t rb, int64_t re, int64_t* first, i
     }
     if (first) *first = f;
     if (count) *count = l - f;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
               void* stream) {
-    if (!c) return PFAAI_ERR_INVALID;
-    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
-    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
-    if ((flags & PFAAI_FLAG_EMIT_JAC) && (!S || !N)) return fail(c, PFAAI_ERR_INVALID, "EMIT_JAC needs S and N");
-    if (!aji && !S && !N) return fail(c, PFAAI_ERR_INVALID, "no output");
+    if (!c) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
+    if ((flags & PFAAI_FLAG_EMIT_JAC) && (!S || !N)) return fail(c, PFAAI_RC_INVALID, "EMIT_JAC needs S and N");
+    if (!aji && !S && !N) return fail(c, PFAAI_RC_INVALID, "no output");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
     // row kernel: default by input, PFAAI_ROWS_KERNEL overrides (A/B runs)
@@ -854,7 +1071,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
             else if (x == "pl512") k = RK_PL512;
             else if (x == "fused") k = RK_FUSED;
             else if (x == "worklist") k = RK_WORKLIST;
-            else return fail(c, PFAAI_ERR_INVALID, "PFAAI_ROWS_KERNEL must be pl, pl512, fused or worklist");
+            else return fail(c, PFAAI_RC_INVALID, "PFAAI_ROWS_KERNEL must be pl, pl512, fused or worklist");
         }
         if (!c->has_g && k != RK_WORKLIST) k = RK_WORKLIST;       // the others walk the G lists
         if (c->max_glen > kPlEntries && k != RK_WORKLIST) k = RK_FUSED;  // lists too long
@@ -867,7 +1084,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         const char* xc = getenv("PFAAI_XCD_CHUNK");
         c->dev.xcd_chunk = xc ? std::max(1, atoi(xc)) : kXcdChunk;
     }
-    if (const char* abl = getenv("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
+    if (const char* abl = DIAG_ENV("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
     // k_rows_pl wave priorities: bit 0 raises the load-issue stages above other
     // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33
     // ms at 10k, tools/gpu/ab_rows.py); PFAAI_PL_PRIO=0..3 overrides (A/B)
@@ -880,7 +1097,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         c->pool_used = 0;
     }
     c->timed = true;
-    if (rb == re) return PFAAI_OK;
+    if (rb == re) return PFAAI_RC_OK;
     switch (c->prob.mode) {
         case 0: return run_mode<0>(c, rb, re, flags, aji, S, N, s);
         case 1: return run_mode<1>(c, rb, re, flags, aji, S, N, s);
@@ -889,8 +1106,8 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
 }
 
 int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int32_t* h_N) {
-    if (!c) return PFAAI_ERR_INVALID;
-    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
+    if (!c) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t np = c->n_pairs;
     int rc;
@@ -909,11 +1126,18 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     if (h_S) HIPCHK(c, hipMemcpyAsync(h_S, S, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (h_N) HIPCHK(c, hipMemcpyAsync(h_N, N, np * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
+}
+
+int pfaai_run_info(const pfaai_ctx* c, int32_t* rows_kernel, int32_t* column_windows) {
+    if (!c) return PFAAI_RC_INVALID;
+    if (rows_kernel) *rows_kernel = c->rows_kernel;
+    if (column_windows) *column_windows = c->windows ? 1 : 0;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_last_stats(pfaai_ctx* c, int64_t* n_events, float* ms_build, float* ms_rows) {
-    if (!c) return PFAAI_ERR_INVALID;
+    if (!c) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     unsigned long long ev = 0;
     HIPCHK(c, hipMemcpy(&ev, static_cast<unsigned long long*>(c->scalars.p) + SC_EVENTS, sizeof(ev),
@@ -927,11 +1151,11 @@ int pfaai_last_stats(pfaai_ctx* c, int64_t* n_events, float* ms_build, float* ms
         if (ms_build) *ms_build = a;
         if (ms_rows) *ms_rows = b;
     }
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_timing(pfaai_ctx* c, int reset, int32_t* n_runs, double* ms_build, double* ms_rows) {
-    if (!c) return PFAAI_ERR_INVALID;
+    if (!c) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     double b = 0.0, r = 0.0;
     const size_t n = c->pool_used / 3;
@@ -951,13 +1175,13 @@ int pfaai_timing(pfaai_ctx* c, int reset, int32_t* n_runs, double* ms_build, dou
         c->pool_used = 0;
         c->timed = false;
     }
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
-    if (!c || !h_counts) return PFAAI_ERR_INVALID;
-    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
-    if (row < 0 || row >= c->n_rows) return fail(c, PFAAI_ERR_INVALID, "row out of range");
+    if (!c || !h_counts) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (row < 0 || row >= c->n_rows) return fail(c, PFAAI_RC_INVALID, "row out of range");
     HIPCHK(c, hipSetDevice(c->device));
     const auto& p = c->prob;
     const int64_t cells = (int64_t)p.n_prot * p.n_ids;
@@ -991,7 +1215,7 @@ int pfaai_debug_row_counts(pfaai_ctx* c, int64_t row, int32_t* h_counts) {
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h_counts, out, cells * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 }  // extern "C"
@@ -1015,13 +1239,13 @@ extern "C" {
 
 int pfaai_debug_div_check(pfaai_ctx* c, int32_t c_max, int32_t d_max, int64_t* mismatches) {
     if (!c || !mismatches || c_max < 1 || d_max < c_max || d_max >= (1 << 24) || c_max > 65535)
-        return PFAAI_ERR_INVALID;
+        return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     int rc = ensure(c, c->dbg, sizeof(unsigned long long));
     if (rc) return rc;
     auto* bad = static_cast<unsigned long long*>(c->dbg.p);
     HIPCHK(c, hipMemsetAsync(bad, 0, sizeof(unsigned long long), c->stream));
-    const char* ns = getenv("PFAAI_DIV_NEWTON");  // diagnostics: check a shorter refinement
+    const char* ns = DIAG_ENV("PFAAI_DIV_NEWTON");  // diagnostics: check a shorter refinement
     if (ns && atoi(ns) == 0)
         hipLaunchKernelGGL(k_div_check<0>, dim3(64, c_max), dim3(256), 0, c->stream, c_max, d_max, bad);
     else if (ns && atoi(ns) == 2)
@@ -1033,52 +1257,52 @@ int pfaai_debug_div_check(pfaai_ctx* c, int32_t c_max, int32_t d_max, int64_t* m
     HIPCHK(c, hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *mismatches = (int64_t)h;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_debug_clocks(pfaai_ctx* c, uint64_t* out, int64_t n) {
-    if (!c || n < 0 || (n > 0 && !out)) return PFAAI_ERR_INVALID;
+    if (!c || n < 0 || (n > 0 && !out)) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t cap = (int64_t)kClkBlocks * 16 * 8;
     if (n == 0) {  // arm: allocate and clear the clock buffer
         int rc = ensure(c, c->dbg, cap * sizeof(uint64_t));
         if (rc) return rc;
         HIPCHK(c, hipMemset(c->dbg.p, 0, cap * sizeof(uint64_t)));
-        return PFAAI_OK;
+        return PFAAI_RC_OK;
     }
-    if (c->dbg.bytes < (size_t)cap * sizeof(uint64_t)) return fail(c, PFAAI_ERR_INVALID, "clocks not armed");
+    if (c->dbg.bytes < (size_t)cap * sizeof(uint64_t)) return fail(c, PFAAI_RC_INVALID, "clocks not armed");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(out, c->dbg.p, std::min(n, cap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_device_alloc(pfaai_ctx* c, void** ptr, int64_t bytes) {
-    if (!c || !ptr || bytes < 0) return PFAAI_ERR_INVALID;
+    if (!c || !ptr || bytes < 0) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMalloc(ptr, bytes > 0 ? bytes : 8));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_device_free(pfaai_ctx* c, void* ptr) {
-    if (!c) return PFAAI_ERR_INVALID;
+    if (!c) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     if (ptr) HIPCHK(c, hipFree(ptr));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_memcpy_d2h(pfaai_ctx* c, void* dst, const void* src, int64_t bytes) {
-    if (!c || bytes < 0) return PFAAI_ERR_INVALID;
+    if (!c || bytes < 0) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 int pfaai_synchronize(pfaai_ctx* c) {
-    if (!c) return PFAAI_ERR_INVALID;
+    if (!c) return PFAAI_RC_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipDeviceSynchronize());
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 
@@ -1088,18 +1312,18 @@ int pfaai_synchronize(pfaai_ctx* c) {
 // context stream while tile k - 1 is copied to pinned host buffer (k-1) & 1
 // on the copy stream and tile k - 2 is handed to the sink on this thread.
 // The run table is built by the first tile only (PFAAI_FLAG_KEEP_RUNS).
-int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,
-                 void* user) {
-    if (!c) return PFAAI_ERR_INVALID;
-    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
-    if (!sink) return fail(c, PFAAI_ERR_INVALID, "sink is required");
-    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
+static int stream_impl(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,
+                       void* user) {
+    if (!c) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (!sink) return fail(c, PFAAI_RC_INVALID, "sink is required");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
     if (c->prob.mode == PFAAI_MODE_QSUB)
-        return fail(c, PFAAI_ERR_INVALID, "pfaai_stream: QSUB rows have no contiguous JAC span (use pfaai_run)");
+        return fail(c, PFAAI_RC_INVALID, "pfaai_stream: QSUB rows have no contiguous JAC span (use pfaai_run)");
     HIPCHK(c, hipSetDevice(c->device));
     const bool jac = flags & PFAAI_FLAG_EMIT_JAC;
     c->st_events = 0;
-    if (rb == re) return PFAAI_OK;
+    if (rb == re) return PFAAI_RC_OK;
     // row tiles: maximal row ranges whose span fits tile_pairs (>= one row)
     std::vector<int64_t> cut{rb};
     int64_t cap = 1;
@@ -1157,7 +1381,7 @@ int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint3
         const int src = sink(user, cut[k], cut[k + 1], f, n, reinterpret_cast<const double*>(hptr(b, 0)),
                              jac ? reinterpret_cast<const double*>(hptr(b, 1)) : nullptr,
                              jac ? reinterpret_cast<const int32_t*>(hptr(b, 2)) : nullptr);
-        return src ? fail(c, src, "pfaai_stream: the sink stopped the stream") : PFAAI_OK;
+        return src ? fail(c, src, "pfaai_stream: the sink stopped the stream") : PFAAI_RC_OK;
     };
     for (int64_t k = 0; k < ntiles; ++k) {
         const int b = (int)(k & 1);
@@ -1185,13 +1409,19 @@ int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint3
     }
     for (int64_t k = std::max<int64_t>(0, ntiles - 2); k < ntiles; ++k)
         if ((rc = deliver(k))) { drain(); return rc; }
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
+}
+
+int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,
+                 void* user) {
+    if (!c) return PFAAI_RC_INVALID;
+    return guarded(c, [&] { return stream_impl(c, rb, re, tile_pairs, flags, sink, user); });
 }
 
 int pfaai_stream_events(const pfaai_ctx* c, int64_t* n_events) {
-    if (!c || !n_events) return PFAAI_ERR_INVALID;
+    if (!c || !n_events) return PFAAI_RC_INVALID;
     *n_events = c->st_events;
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 
@@ -1199,22 +1429,22 @@ int pfaai_stream_events(const pfaai_ctx* c, int64_t* n_events) {
 // scp_db.hpp:161-262): count Lc / T, stable LSD radix sort of the triples by
 // tetramer * P + protein (8-bit digits, the work-list sort's kernels), split
 // the sorted (protein, genome) records into the F columns.
-int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, const int32_t* tetra, int64_t n,
-                  int32_t n_prot, int32_t n_genome, int32_t* Lc_out, int64_t* Lp_out, int32_t* F_prot_out,
-                  int32_t* F_genome_out, int32_t* T_out) {
-    if (!c) return PFAAI_ERR_INVALID;
+static int build_f_impl(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, const int32_t* tetra, int64_t n,
+                        int32_t n_prot, int32_t n_genome, int32_t* Lc_out, int64_t* Lp_out, int32_t* F_prot_out,
+                        int32_t* F_genome_out, int32_t* T_out) {
+    if (!c) return PFAAI_RC_INVALID;
     if (n < 0 || n > kMaxF || n_prot < 1 || n_prot >= kMaxRuns || n_genome < 1)
-        return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: bad sizes (|F| <= 2^32 - 64, 1 <= n_prot < 4096)");
+        return fail(c, PFAAI_RC_INVALID, "pfaai_build_f: bad sizes (|F| <= 2^32 - 64, 1 <= n_prot < 4096)");
     if ((n && (!prot || !genome || !tetra || !F_prot_out || !F_genome_out)) || !Lc_out || !Lp_out)
-        return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: null array");
+        return fail(c, PFAAI_RC_INVALID, "pfaai_build_f: null array");
     {  // ranges, and every protein's triples in non-decreasing genome order (the stable sort keeps it)
         std::vector<int32_t> last(n_prot, -1);
         for (int64_t i = 0; i < n; ++i) {
             const int32_t p = prot[i], g = genome[i], t = tetra[i];
             if (p < 0 || p >= n_prot || g < 0 || g >= n_genome || t < 0 || t >= PFAAI_NTETRAMERS)
-                return fail(c, PFAAI_ERR_INVALID, "pfaai_build_f: protein, genome or tetramer id out of range");
+                return fail(c, PFAAI_RC_INVALID, "pfaai_build_f: protein, genome or tetramer id out of range");
             if (g < last[p])
-                return fail(c, PFAAI_ERR_INVALID,
+                return fail(c, PFAAI_RC_INVALID,
                             "pfaai_build_f: triples of a protein must come in non-decreasing genome order");
             last[p] = g;
         }
@@ -1223,18 +1453,14 @@ int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, cons
     hipStream_t s = c->stream;
     int rc;
     const int64_t nn = std::max<int64_t>(n, 1);
-    const int64_t ntiles = ceil_div(nn, kRsTile), hist_n = kRsBins * ntiles;
     DevBuf in_p, in_g, in_t, Tdev;
-    auto cleanup = [&]() { release(in_p); release(in_g); release(in_t); release(Tdev); };
+    auto cleanup = [&]() { release(in_p); release(in_g); release(in_t); release(Tdev); release_sort_space(c); };
     if ((rc = upload(c, in_p, prot, n)) || (rc = upload(c, in_g, genome, n)) || (rc = upload(c, in_t, tetra, n))) {
         cleanup();
         return rc;
     }
-    if ((rc = ensure(c, c->key_c, nn * 4)) || (rc = ensure(c, c->key_a, nn * 4)) || (rc = ensure(c, c->key_b, nn * 4)) ||
-        (rc = ensure(c, c->val_a, nn * 4)) || (rc = ensure(c, c->val_b, nn * 4)) || (rc = ensure(c, c->rec_c, nn * 8)) ||
-        (rc = ensure(c, c->recs, nn * 8)) || (rc = ensure(c, c->hist, hist_n * 4)) ||
-        (rc = ensure(c, c->hoff, (hist_n + 1) * 8)) || (rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * 4)) ||
-        (rc = ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max<int64_t>(hist_n, PFAAI_NTETRAMERS), kScanTile)) * 8))) {
+    if ((rc = ensure(c, c->key_c, nn * 4)) || (rc = ensure(c, c->rec_c, nn * 8)) || (rc = ensure(c, c->recs, nn * 8)) ||
+        (rc = ensure(c, c->cnt_t, PFAAI_NTETRAMERS * 4)) || (rc = ensure_sort_space(c, n))) {
         cleanup();
         return rc;
     }
@@ -1253,38 +1479,13 @@ int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, cons
     HIPCHK(c, hipGetLastError());
     auto* recs = static_cast<uint2*>(c->recs.p);
     if (n) {
-        int bits = 1;
-        while (bits < 32 && ((int64_t)1 << bits) < (int64_t)PFAAI_NTETRAMERS * n_prot) ++bits;
-        const int passes = (bits + 7) / 8;
-        auto* hist = static_cast<uint32_t*>(c->hist.p);
-        auto* hoff = static_cast<unsigned long long*>(c->hoff.p);
-        uint32_t* kin = keys0;
-        uint32_t* vin = nullptr;
-        uint32_t* kout = static_cast<uint32_t*>(c->key_a.p);
-        uint32_t* vout = static_cast<uint32_t*>(c->val_a.p);
-        uint32_t* kalt = static_cast<uint32_t*>(c->key_b.p);
-        uint32_t* valt = static_cast<uint32_t*>(c->val_b.p);
-        for (int pass = 0; pass < passes; ++pass) {
-            const int shift = 8 * pass;
-            const bool first = pass == 0, last = pass == passes - 1;
-            hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kRsThreads), 0, s, kin, n, shift, hist, ntiles);
-            if ((rc = scan_u32(c, hist, hist_n, hoff, s))) { cleanup(); return rc; }
-#define RS(F, L)                                                                                                  \
-    hipLaunchKernelGGL((k_rs_scatter<F, L>), dim3(ntiles), dim3(kRsThreads), 0, s, kin, vin, n, shift, hoff, hist, \
-                       ntiles, kout, vout, rec0, recs)
-            if (first && last) RS(true, true);
-            else if (first) RS(true, false);
-            else if (last) RS(false, true);
-            else RS(false, false);
-#undef RS
-            kin = kout;
-            vin = vout;
-            std::swap(kout, kalt);
-            std::swap(vout, valt);
+        if ((rc = radix_sort_recs(c, keys0, n, bits_for((int64_t)PFAAI_NTETRAMERS * n_prot), rec0, recs, s, nullptr))) {
+            cleanup();
+            return rc;
         }
         // the F columns into two free key-sized buffers
-        int32_t* fp = reinterpret_cast<int32_t*>(kout);
-        int32_t* fg = reinterpret_cast<int32_t*>(vout);
+        int32_t* fp = static_cast<int32_t*>(c->key_a.p);
+        int32_t* fg = static_cast<int32_t*>(c->key_b.p);
         hipLaunchKernelGGL(k_f_split, dim3(grid), dim3(256), 0, s, recs, n, fp, fg);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(F_prot_out, fp, n * 4, hipMemcpyDeviceToHost, s));
@@ -1294,28 +1495,36 @@ int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, cons
     HIPCHK(c, hipMemcpyAsync(lc.data(), cnt, PFAAI_NTETRAMERS * 4, hipMemcpyDeviceToHost, s));
     if (T_out) HIPCHK(c, hipMemcpyAsync(T_out, Tdev.p, tbytes, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    cleanup();
-    c->wl_ready = false;  // the work-list buffers were resized / overwritten
+    cleanup();  // also the work-list buffers: a later work-list run re-allocates them
     Lp_out[0] = 0;
     for (int t = 0; t < PFAAI_NTETRAMERS; ++t) {
         Lc_out[t] = (int32_t)lc[t];
         Lp_out[t + 1] = Lp_out[t] + lc[t];
     }
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
+
+int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, const int32_t* tetra, int64_t n,
+                  int32_t n_prot, int32_t n_genome, int32_t* Lc_out, int64_t* Lp_out, int32_t* F_prot_out,
+                  int32_t* F_genome_out, int32_t* T_out) {
+    if (!c) return PFAAI_RC_INVALID;
+    return guarded(c, [&] {
+        return build_f_impl(c, prot, genome, tetra, n, n_prot, n_genome, Lc_out, Lp_out, F_prot_out, F_genome_out, T_out);
+    });
+}
 
 // Rows into host arrays at their JAC span: one thread per context (device)
 // runs its own row block; the spans of disjoint row blocks are disjoint in
 // ALL and QT, so several devices fill one host JAC array without a gather.
 int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* h_aji, double* h_S,
                        int32_t* h_N) {
-    if (!c) return PFAAI_ERR_INVALID;
-    if (!c->loaded) return fail(c, PFAAI_ERR_INVALID, "no problem loaded");
-    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_ERR_INVALID, "row range out of bounds");
+    if (!c) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
     if (c->prob.mode == PFAAI_MODE_QSUB && !(rb == 0 && re == c->n_rows))
-        return fail(c, PFAAI_ERR_INVALID, "pfaai_compute_rows: QSUB row blocks have no contiguous JAC span");
-    if (rb == re) return PFAAI_OK;
+        return fail(c, PFAAI_RC_INVALID, "pfaai_compute_rows: QSUB row blocks have no contiguous JAC span");
+    if (rb == re) return PFAAI_RC_OK;
     HIPCHK(c, hipSetDevice(c->device));
     int64_t f = 0, n = 0;
     pfaai_row_span(c, rb, re, &f, &n);
@@ -1337,7 +1546,7 @@ int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, dou
     if (h_S) HIPCHK(c, hipMemcpyAsync(h_S + f, S, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (h_N) HIPCHK(c, hipMemcpyAsync(h_N + f, N, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return PFAAI_OK;
+    return PFAAI_RC_OK;
 }
 
 }  // extern "C"

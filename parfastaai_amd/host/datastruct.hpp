@@ -22,6 +22,7 @@ class DataBase {
   public:
     using JACType = JACTuple;
     DataBase(DBMetaData meta, LoadedArrays arr) : m_meta(std::move(meta)), m_arr(std::move(arr)) {
+        if (m_arr.Lc.empty()) m_arr.Lc.assign(kNTetramers, 0);  // G path: F is built on the device
         m_Lp.assign(kNTetramers, 0);
         int32_t run = 0;
         for (int t = 0; t < kNTetramers; ++t) {  // parallelPrefixSum, ds_helper.hpp:112-122
@@ -33,6 +34,9 @@ class DataBase {
     const std::vector<int32_t>& refLp() const { return m_Lp; }
     const std::vector<DPair>& refF() const { return m_arr.F; }
     const DMatrix& refT() const { return m_arr.T; }
+    // genome-major `<p>_genomes` lists (G path; empty on the F path)
+    const std::vector<int64_t>& refGOff() const { return m_arr.G_off; }
+    const std::vector<int32_t>& refGTet() const { return m_arr.G_tet; }
     const DBMetaData& meta() const { return m_meta; }
 
   protected:
@@ -131,6 +135,7 @@ class QTData : public DataBase {
     int64_t qrySetSize() const { return (int64_t)m_meta.qyGenomeSet.size(); }
     int64_t tgtSetSize() const { return (int64_t)m_meta.genomeSet.size(); }
     int64_t nGenomePairs() const { return qrySetSize() * tgtSetSize(); }
+    int64_t nUnionGenomes() const { return qrySetSize() + tgtSetSize(); }  // ds_impl.hpp:370
     bool isQryGenome(int32_t g) const { return g >= tgtSetSize(); }
     int32_t mapQueryId(int32_t g) const { return g < tgtSetSize() ? g : (int32_t)(g - tgtSetSize()); }
     int32_t mapTargetId(int32_t g) const { return mapQueryId(g); }

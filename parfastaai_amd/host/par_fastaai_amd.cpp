@@ -4,6 +4,15 @@
 //   par_fastaai_amd [-r query_db] [-s sep] [-q query_list] in_db out_csv
 //                   [--ref-compat] [--device N] [--bin PREFIX]
 //
+// Ingest reads the `<p>_genomes` blobs (genome-major lists G) and pfaai_load
+// builds F on the device (stable radix sort), so the run takes the
+// benchmarked k_blk + k_rows_pl path; `--loader tetras` reads F from the
+// `<p>_tetras` tables instead (the reference's own F; G is then built on the
+// device).  Default semantics are the corrected ones:
+// a pair sharing no tetramer gets AJI 0, and -r divides by the query's and
+// the target's own tetramer counts; --ref-compat reproduces the reference's
+// values for those cells bit for bit.  Every other cell is identical.
+//
 // Same options, same mode dispatch (main.cpp:337-356), same validation
 // errors and exit codes (3 for a bad -q list or overlapping -r genomes,
 // main.cpp:204-300; 105 / 106 / 109 for option validation / missing
@@ -45,6 +54,8 @@ struct AppParams {  // main.cpp:56-131
     std::string streamAji;       // --stream-aji FILE: pfaai_stream the AJI vector to FILE (no CSV)
     long long tilePairs = 1ll << 27;
     std::vector<int> devices;    // --devices 0,1,...: one context per device, rows split (ALL / QT)
+    bool loaderTetras = false;   // --loader tetras: F from `<p>_tetras` (else G from `<p>_genomes`)
+    std::string dumpGenomes;     // --dump-genomes PREFIX: write the G-path arrays (G_off, G_tet, T) and exit
 
     void print() const {
         std::vector<std::string> args = {" Input Database  : " + pathToDatabase + " ",
@@ -84,7 +95,10 @@ const char* kUsage =
     "  -r,--query_db TEXT:FILE  Path to the Query Database [Optional (default: Same as the Input DB)]\n"
     "  -s,--separator TEXT [,]  Field Separator in the output file [Optional (default: ,)].\n"
     "  -q,--query_subset TEXT:FILE  Path to Query List (Should be subset of genomoes in the input DB.)\n"
-    "  --ref-compat             Reproduce the reference's quirks (zero-overlap pairs, QT T indexing)\n"
+    "  --ref-compat             Reproduce the reference's values where it has quirks: pairs sharing no\n"
+    "                           tetramer (default: AJI 0) and -r denominators (default: the query's and\n"
+    "                           the target's own counts).  All other cells are identical either way.\n"
+    "  --loader TEXT [genomes]  genomes: read <p>_genomes, F built on the GPU; tetras: read <p>_tetras\n"
     "  --device INT [0]         HIP device\n"
     "  --devices LIST           Comma-separated HIP devices: rows split over them (all-vs-all, -r)\n"
     "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n"
@@ -140,6 +154,16 @@ int parse(int argc, char** argv, AppParams& a) {
             if (!value(v)) return 114;
             a.tilePairs = std::atoll(v.c_str());
             if (a.tilePairs < 1) return 105;
+        } else if (is("--loader", "--loader")) {
+            std::string v;
+            if (!value(v)) return 114;
+            if (v != "genomes" && v != "tetras") {
+                std::cerr << "--loader: " << v << " not in {genomes, tetras}\nRun with --help for more information.\n";
+                return 105;
+            }
+            a.loaderTetras = v == "tetras";
+        } else if (is("--dump-genomes", "--dump-genomes")) {
+            if (!value(a.dumpGenomes)) return 114;
         } else if (is("--bin", "--bin")) {
             if (!value(a.binPrefix)) return 114;
         } else if (is("--dump-arrays", "--dump-arrays")) {
@@ -210,6 +234,54 @@ int dump_arrays(const std::string& prefix, const LoadedArrays& arr) {
     return ok ? 0 : 1;
 }
 
+// --dump-genomes: the G-path arrays (cereal vector<int64> G_off, vector<int>
+// G_tet, DMatrix<int> T), no GPU.
+int dump_genomes(const std::string& prefix, const LoadedArrays& arr) {
+    auto put = [](FILE* f, const void* p, std::size_t n) { return std::fwrite(p, 1, n, f) == n; };
+    bool ok = true;
+    if (FILE* f = std::fopen((prefix + "_g_off.bin").c_str(), "wb")) {
+        uint64_t n = arr.G_off.size();
+        ok &= put(f, &n, 8) && put(f, arr.G_off.data(), 8 * n);
+        std::fclose(f);
+    } else ok = false;
+    if (FILE* f = std::fopen((prefix + "_g_tet.bin").c_str(), "wb")) {
+        uint64_t n = arr.G_tet.size();
+        ok &= put(f, &n, 8) && put(f, arr.G_tet.data(), 4 * n);
+        std::fclose(f);
+    } else ok = false;
+    if (FILE* f = std::fopen((prefix + "_t_matrix.bin").c_str(), "wb")) {
+        uint64_t h[3] = {arr.T.rows(), arr.T.cols(), arr.T.rows() * arr.T.cols()};
+        ok &= put(f, h, 24) && put(f, arr.T.data.data(), 4 * arr.T.data.size());
+        std::fclose(f);
+    } else ok = false;
+    return ok ? 0 : 1;
+}
+
+const char* kRowsKernelName[] = {"k_rows_pl", "k_rows_pl512", "k_rows(fused)", "k_rows(worklist)"};
+
+// The loader: G from `<p>_genomes` unless --loader tetras / --dump-arrays, or
+// a blob that is not a set (then the `<p>_tetras` F, as the reference reads).
+template <class LoadG, class LoadF>
+int ingest(const AppParams& app, LoadG load_g, LoadF load_f, DBMetaData& meta, LoadedArrays& arr, std::string& err) {
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = -1;
+    const char* what = "<p>_genomes -> G";
+    if (!app.loaderTetras && app.dumpPrefix.empty()) rc = load_g(meta, arr, err);
+    if (rc == -1) {
+        meta = DBMetaData();
+        arr = LoadedArrays();
+        rc = load_f(meta, arr, err);
+        what = "<p>_tetras -> F";
+    }
+    if (rc) {
+        std::cerr << err << std::endl;
+        return rc;
+    }
+    std::printf("Load (SQLite)       : %10.2f ms  (%s, %zu entries)\n", ms_since(t0), what,
+                arr.F.empty() ? arr.G_tet.size() : arr.F.size());
+    return 0;
+}
+
 template <typename DS>
 int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
     auto t0 = std::chrono::steady_clock::now();
@@ -219,18 +291,22 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         if (!app.streamAji.empty()) {  // output-tile streaming: no CSV, no whole matrix anywhere
             if (mode == PFAAI_MODE_QSUB) {
                 std::cerr << "--stream-aji does not support -q" << std::endl;
-                return PFAAI_ERR_INVALID;
+                return PFAAI_RC_INVALID;
             }
             int rc = impl.streamAJI(app.streamAji, app.tilePairs);
             std::printf("AJI stream (MI355X) : %10.2f ms  (|E| = %lld) -> %s\n", ms_since(t0),
                         (long long)impl.nEvents(), app.streamAji.c_str());
             return rc;
         }
-        impl.run();
-        std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; run tables %.2f ms, rows %.2f ms)\n",
-                    impl.nDevices(), ms_since(t0), (long long)impl.nEvents(), impl.msBuild(), impl.msRows());
-        if (app.pathToOutputFile.empty()) return 0;
         auto t1 = std::chrono::steady_clock::now();
+        impl.run();
+        const int rk = impl.rowsKernel();
+        std::printf("AJI (MI355X x%d)     : %10.2f ms  (load %.2f ms; |E| = %lld; %s: run tables %.2f ms, rows %.2f ms)\n",
+                    impl.nDevices(), ms_since(t0), std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    (long long)impl.nEvents(), rk >= 0 && rk < 4 ? kRowsKernelName[rk] : "?", impl.msBuild(),
+                    impl.msRows());
+        if (app.pathToOutputFile.empty()) return 0;
+        t1 = std::chrono::steady_clock::now();
         std::printf("Writing output with %lld query genomes and %lld target genomes. \n",
                     (long long)ds.qrySetSize(), (long long)ds.tgtSetSize());
         auto M = dense_matrix(ds, impl.getJAC(), impl.getAJI(), isSubset);
@@ -252,13 +328,13 @@ int parallel_fastaai(const AppParams& app) {  // main.cpp:177-202
     DBMetaData meta;
     LoadedArrays arr;
     std::string err;
-    auto t0 = std::chrono::steady_clock::now();
-    if (int rc = load_single(app.pathToDatabase, meta, arr, err)) {
-        std::cerr << err << std::endl;
+    const std::string& db = app.pathToDatabase;
+    if (int rc = ingest(
+            app, [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_single_g(db, m, a, e); },
+            [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_single(db, m, a, e); }, meta, arr, err))
         return rc;
-    }
-    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
     if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
+    if (!app.dumpGenomes.empty()) return dump_genomes(app.dumpGenomes, arr);
     AllData ds(std::move(meta), std::move(arr));
     return run_and_print(ds, PFAAI_MODE_ALL, app, true);
 }
@@ -284,14 +360,14 @@ int parallel_subset_fastaai(const AppParams& app) {  // main.cpp:234-266
     DBMetaData meta;
     LoadedArrays arr;
     std::string err;
-    auto t0 = std::chrono::steady_clock::now();
-    if (int rc = load_single(app.pathToDatabase, meta, arr, err)) {
-        std::cerr << err << std::endl;
+    const std::string& db = app.pathToDatabase;
+    if (int rc = ingest(
+            app, [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_single_g(db, m, a, e); },
+            [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_single(db, m, a, e); }, meta, arr, err))
         return rc;
-    }
     if (validate_subset(app, meta)) return 3;
-    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
     if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
+    if (!app.dumpGenomes.empty()) return dump_genomes(app.dumpGenomes, arr);
     QSubData ds(std::move(meta), std::move(arr), app.qryGenomeSet);
     return run_and_print(ds, PFAAI_MODE_QSUB, app, true);
 }
@@ -319,14 +395,15 @@ int parallel_qry2tgt_fastaai(const AppParams& app) {  // main.cpp:302-335
     DBMetaData meta;
     LoadedArrays arr;
     std::string err;
-    auto t0 = std::chrono::steady_clock::now();
-    if (int rc = load_qt(app.pathToDatabase, app.pathToQryDatabase, meta, arr, err)) {
-        std::cerr << err << std::endl;
+    const std::string &tdb = app.pathToDatabase, &qdb = app.pathToQryDatabase;
+    if (int rc = ingest(
+            app, [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_qt_g(tdb, qdb, m, a, e); },
+            [&](DBMetaData& m, LoadedArrays& a, std::string& e) { return load_qt(tdb, qdb, m, a, e); }, meta, arr,
+            err))
         return rc;
-    }
     if (validate_qry2tgt(meta)) return 3;
-    std::printf("Load (SQLite -> F)  : %10.2f ms  (|F| = %zu)\n", ms_since(t0), arr.F.size());
     if (!app.dumpPrefix.empty()) return dump_arrays(app.dumpPrefix, arr);
+    if (!app.dumpGenomes.empty()) return dump_genomes(app.dumpGenomes, arr);
     QTData ds(std::move(meta), std::move(arr));
     return run_and_print(ds, PFAAI_MODE_QT, app, false);
 }

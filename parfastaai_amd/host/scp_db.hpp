@@ -5,10 +5,18 @@
 //   SQLiteHelper        include/pfaai/db_helper.hpp:33-219
 //   SQLiteSCPDataBase   include/pfaai/scp_db.hpp:59-263
 //   QTSQLiteSCPDataBase include/pfaai/scp_db.hpp:267-590
-// Instead of one giant UNION ALL ... ORDER BY per thread (scp_db.hpp:161-216)
-// every protein's `<p>_tetras` table is read by its own read-only connection
-// in parallel (OpenMP) and F is assembled by a stable counting sort on the
-// tetramer id -- the same (tetramer, protein, blob order) layout.
+// Two ingest paths, both parallel over proteins (one read-only connection
+// per OpenMP thread):
+//   load_*_g  (the default, north_star's device F build): every protein's
+//             `<p>_genomes` table -- the blobs the reference reads only the
+//             lengths of for T (scp_db.hpp:219-262) -- becomes the genome-
+//             major lists G (CSR over (genome, protein)); F is then built on
+//             the device by pfaai_load (a stable radix sort), never on the
+//             host.  No UNION ALL, no ORDER BY.
+//   load_*    (--dump-arrays, and the fallback when a `<p>_genomes` blob is
+//             not a set): every protein's `<p>_tetras` table, F assembled by a
+//             stable counting sort on the tetramer id -- the reference's
+//             (tetramer, protein, blob order) layout of scp_db.hpp:161-216.
 #pragma once
 #include <omp.h>
 
@@ -44,9 +52,11 @@ struct DBMetaData {
 };
 
 struct LoadedArrays {
-    std::vector<int32_t> Lc;
-    std::vector<DPair> F;
+    std::vector<int32_t> Lc;  // F path only
+    std::vector<DPair> F;     // F path only
     DMatrix T;
+    std::vector<int64_t> G_off;  // G path only: [n_ids * P + 1], list (g, p) at g * P + p
+    std::vector<int32_t> G_tet;  // G path only: ascending tetramers of each list
 };
 
 class Conn {
@@ -122,7 +132,7 @@ inline int load_single(const std::string& path, DBMetaData& meta, LoadedArrays& 
     Conn c(path);
     if (!c.ok()) {
         err = "Error in opening " + path + ": " + c.error();
-        return 1;  // PFAAI_ERR_SQLITE_DB
+        return 1;  // PFAAI_RC_SQLITE_DB
     }
     int e = 0;
     meta.proteinSet = column_strings(c, "SELECT DISTINCT scp_acc FROM scp_data", &e);  // db_helper.hpp:195-215
@@ -173,7 +183,7 @@ inline int load_single(const std::string& path, DBMetaData& meta, LoadedArrays& 
             bad = 1;
             break;
         }
-    if (bad) return 3;  // PFAAI_ERR_CONSTRUCT
+    if (bad) return 3;  // PFAAI_RC_CONSTRUCT
     assemble_f(rows, out);
     return 0;
 }
@@ -255,6 +265,180 @@ inline int load_qt(const std::string& tgt, const std::string& qry, DBMetaData& m
             return 3;
         }
     assemble_f(rows, out);
+    return 0;
+}
+
+
+// ---------------------------------------------------------------------------
+// G path: `<p>_genomes` (genome_id INTEGER PK, tetramers BLOB int32[]).
+// ---------------------------------------------------------------------------
+struct ProteinLists {  // one protein's lists, in table order
+    std::vector<int32_t> gid, len, tet;
+    int err = SQLITE_OK;
+};
+
+// Read `<schema>.<acc>_genomes` into r, genome ids offset by id_base and
+// checked against [0, n_ids_db); T(p, id_base + gid) = list length.
+inline int read_genome_lists(Conn& tc, const std::string& schema, const std::string& acc, int32_t id_base,
+                             int32_t n_ids_db, ProteinLists& r) {
+    return tc.each("SELECT genome_id, tetramers FROM " + schema + "`" + acc + "_genomes`", [&](sqlite3_stmt* st) {
+        const int gid = sqlite3_column_int(st, 0);
+        const int nb = sqlite3_column_bytes(st, 1) / 4;
+        const auto* t = static_cast<const int32_t*>(sqlite3_column_blob(st, 1));
+        if (gid < 0 || gid >= n_ids_db) {
+            r.err = 1;
+            return;
+        }
+        r.gid.push_back(id_base + gid);
+        r.len.push_back(nb);
+        r.tet.insert(r.tet.end(), t, t + nb);
+    });
+}
+
+// Sort each list (a blob is normally ascending already) and check that it
+// is a set of valid tetramer ids.  false: a duplicate or an id out of range
+// (the caller falls back to the `<p>_tetras` path, which reads F as stored).
+inline bool normalise_lists(ProteinLists& r) {
+    std::size_t off = 0;
+    for (std::size_t k = 0; k < r.gid.size(); ++k) {
+        int32_t* b = r.tet.data() + off;
+        int32_t* e = b + r.len[k];
+        if (!std::is_sorted(b, e)) std::sort(b, e);
+        for (int32_t* x = b; x < e; ++x)
+            if (*x < 0 || *x >= kNTetramers || (x > b && *x == x[-1])) return false;
+        off += r.len[k];
+    }
+    return true;
+}
+
+// CSR over (genome, protein) from per-protein lists; T from the lengths.
+inline void assemble_g(std::vector<ProteinLists>& lists, int32_t n_ids, LoadedArrays& out) {
+    const int64_t P = (int64_t)lists.size();
+    out.G_off.assign((int64_t)n_ids * P + 1, 0);
+    for (int64_t p = 0; p < P; ++p)
+        for (std::size_t k = 0; k < lists[p].gid.size(); ++k) {
+            out.G_off[(int64_t)lists[p].gid[k] * P + p + 1] = lists[p].len[k];
+            out.T((std::size_t)p, (std::size_t)lists[p].gid[k]) = lists[p].len[k];
+        }
+    for (int64_t k = 0; k < (int64_t)n_ids * P; ++k) out.G_off[k + 1] += out.G_off[k];
+    out.G_tet.resize(out.G_off.back());
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t p = 0; p < P; ++p) {
+        std::size_t off = 0;
+        for (std::size_t k = 0; k < lists[p].gid.size(); ++k) {
+            std::copy(lists[p].tet.begin() + off, lists[p].tet.begin() + off + lists[p].len[k],
+                      out.G_tet.begin() + out.G_off[(int64_t)lists[p].gid[k] * P + p]);
+            off += lists[p].len[k];
+        }
+        std::vector<int32_t>().swap(lists[p].gid);
+        std::vector<int32_t>().swap(lists[p].tet);
+    }
+}
+
+// SQLiteSCPDataBase metadata + `<p>_genomes` lists.  Returns 0, an error
+// code (1 SQLite, 3 construct), or -1: a blob is not a set (use load_single).
+inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays& out, std::string& err) {
+    Conn c(path);
+    if (!c.ok()) {
+        err = "Error in opening " + path + ": " + c.error();
+        return 1;  // PFAAI_RC_SQLITE_DB
+    }
+    int e = 0;
+    meta.proteinSet = column_strings(c, "SELECT DISTINCT scp_acc FROM scp_data", &e);  // db_helper.hpp:195-215
+    if (e == SQLITE_OK) meta.genomeSet = column_strings(c, "SELECT genome_name FROM genome_metadata", &e);
+    if (e != SQLITE_OK) {
+        err = "Error in reading metadata of " + path + ": " + c.error();
+        return 1;
+    }
+    const int P = (int)meta.proteinSet.size();
+    const int G = (int)meta.genomeSet.size();
+    std::vector<ProteinLists> lists(P);
+    std::vector<char> sets(P, 1);
+#pragma omp parallel
+    {
+        Conn tc(path);
+#pragma omp for schedule(dynamic, 1)
+        for (int p = 0; p < P; ++p) {
+            auto& r = lists[p];
+            if (!tc.ok()) {
+                r.err = 1;
+                continue;
+            }
+            const int rc = read_genome_lists(tc, "", meta.proteinSet[p], 0, G, r);
+            if (rc != SQLITE_OK) r.err = rc;
+            if (!r.err) sets[p] = normalise_lists(r);
+        }
+    }
+    for (int p = 0; p < P; ++p)
+        if (lists[p].err) {
+            err = "Error in reading tables of protein " + meta.proteinSet[p] + " from " + path;
+            return 3;  // PFAAI_RC_CONSTRUCT
+        }
+    for (int p = 0; p < P; ++p)
+        if (!sets[p]) return -1;
+    out.T = DMatrix(P, G);
+    assemble_g(lists, G, out);
+    return 0;
+}
+
+// QTSQLiteSCPDataBase metadata + both DBs' `<p>_genomes` lists over the
+// shared proteins (db_helper.hpp:109-166); query ids offset by nT.  F built
+// from these holds every tetramer of either DB; the reference's inner join
+// (scp_db.hpp:459-466) keeps only those in both -- the rest form runs with
+// no query-target pair, so counts, S, N and |E| are the same.
+inline int load_qt_g(const std::string& tgt, const std::string& qry, DBMetaData& meta, LoadedArrays& out,
+                     std::string& err) {
+    Conn c(tgt);
+    if (!c.ok()) {
+        err = "Error in opening " + tgt + ": " + c.error();
+        return 1;
+    }
+    if (c.exec("ATTACH DATABASE '" + qry + "' as QueryDB ;") != SQLITE_OK) {
+        err = "Error in attaching query database : " + qry + ": " + c.error();
+        return 1;
+    }
+    int e = 0;
+    meta.proteinSet = column_strings(c,
+                                     "SELECT DISTINCT target_table.scp_acc \n"
+                                     "  FROM `main`.scp_data as target_table, `QueryDB`.scp_data as query_table \n"
+                                     "  WHERE target_table.scp_acc = query_table.scp_acc;",
+                                     &e);
+    if (e == SQLITE_OK) meta.genomeSet = column_strings(c, "SELECT genome_name FROM `main`.genome_metadata", &e);
+    if (e == SQLITE_OK) meta.qyGenomeSet = column_strings(c, "SELECT genome_name FROM `QueryDB`.genome_metadata", &e);
+    if (e != SQLITE_OK) {
+        err = "Error in reading metadata: " + c.error();
+        return 1;
+    }
+    const int P = (int)meta.proteinSet.size();
+    const int nT = (int)meta.genomeSet.size(), nQ = (int)meta.qyGenomeSet.size();
+    std::vector<ProteinLists> lists(P);
+    std::vector<char> sets(P, 1);
+#pragma omp parallel
+    {
+        Conn tc(tgt);
+        const bool ok = tc.ok() && tc.exec("ATTACH DATABASE '" + qry + "' as QueryDB ;") == SQLITE_OK;
+#pragma omp for schedule(dynamic, 1)
+        for (int p = 0; p < P; ++p) {
+            auto& r = lists[p];
+            if (!ok) {
+                r.err = 1;
+                continue;
+            }
+            int rc = read_genome_lists(tc, "main.", meta.proteinSet[p], 0, nT, r);
+            if (rc == SQLITE_OK) rc = read_genome_lists(tc, "QueryDB.", meta.proteinSet[p], nT, nQ, r);
+            if (rc != SQLITE_OK) r.err = rc;
+            if (!r.err) sets[p] = normalise_lists(r);
+        }
+    }
+    for (int p = 0; p < P; ++p)
+        if (lists[p].err) {
+            err = "Error in reading tables of protein " + meta.proteinSet[p];
+            return 3;
+        }
+    for (int p = 0; p < P; ++p)
+        if (!sets[p]) return -1;
+    out.T = DMatrix(P, nT + nQ);
+    assemble_g(lists, nT + nQ, out);
     return 0;
 }
 

@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert _capi.load_library().pfaai_version() == 3
+    assert _capi.load_library().pfaai_version() == 4
 
 
 def test_problem_struct_layout():
@@ -55,3 +55,15 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
                 txt = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "import oracle" not in txt and "pfaai_oracle" not in txt, f
+
+
+def test_release_library_ignores_diagnostic_switches():
+    """The result-changing ablations and the stage-clock instrumentation
+    (PFAAI_ABLATE, PFAAI_BLK_ABLATE, PFAAI_PL_CLK, PFAAI_DIV_NEWTON) exist
+    only in libpfaai_hip_diag.so (-DPFAAI_DIAGNOSTICS): the release library
+    does not even contain their names, so no environment can change its
+    results."""
+    blob = open(_capi.LIB_PATH, "rb").read()
+    for name in (b"PFAAI_ABLATE", b"PFAAI_BLK_ABLATE", b"PFAAI_PL_CLK", b"PFAAI_DIV_NEWTON"):
+        assert name not in blob, name
+    assert b"PFAAI_ROWS_KERNEL" in blob  # result-preserving variant switches stay

@@ -97,3 +97,69 @@ def test_fmt_rule_on_fixture_csv():
         for line in text(name).splitlines()[1:]:
             for cell in line.split(",")[1:]:
                 assert fm.fmt_double(float(cell)) == cell
+
+
+def _f_from_g(G_off, G_tet, n_ids, P):
+    """F (protein, genome) ordered by (tetramer, protein, genome) and Lc from
+    genome-major lists: the host statement of what pfaai_load builds on the
+    device from G (stable sort by tetramer * P + protein)."""
+    lens = np.diff(G_off)
+    lst = np.repeat(np.arange(n_ids * P, dtype=np.int64), lens)
+    g, p = lst // P, lst % P
+    t = G_tet.astype(np.int64)
+    order = np.lexsort((g, p, t))
+    F = np.stack([p[order], g[order]], axis=1).astype(np.int32)
+    return F, np.bincount(t, minlength=160000).astype(np.int32)
+
+
+def _read_i64_vec(path):
+    raw = open(path, "rb").read()
+    n = struct.unpack("<Q", raw[:8])[0]
+    return np.frombuffer(raw[8:8 + 8 * n], dtype=np.int64)
+
+
+@pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
+def test_genomes_loader_gives_reference_f(tmp_path, name):
+    """The default ingest (`<p>_genomes` -> G): F built from G equals the
+    reference's F fixture, Lc and T too (the GPU does this build)."""
+    db = unpack(tmp_path, name + ".db")
+    pre = str(tmp_path / "g")
+    r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", pre)
+    assert r.returncode == 0, r.stderr
+    assert "<p>_genomes -> G" in r.stdout
+    G_off, G_tet = _read_i64_vec(pre + "_g_off.bin"), fm.read_vec_i32(pre + "_g_tet.bin")
+    T = fm.read_matrix_i32(pre + "_t_matrix.bin")
+    P, n = T.shape
+    assert len(G_off) == n * P + 1 and G_off[-1] == len(G_tet)
+    for k in range(n * P):  # strictly ascending lists
+        assert (np.diff(G_tet[G_off[k]:G_off[k + 1]]) > 0).all()
+    F, Lc = _f_from_g(G_off, G_tet, n, P)
+    assert np.array_equal(F, fm.read_f_array(gpath(name + "_f_array.bin")))
+    assert np.array_equal(Lc, fm.read_vec_i32(gpath(name + "_lc_array.bin")))
+    assert np.array_equal(T, fm.read_matrix_i32(gpath(name + "_t_matrix.bin")))
+
+
+def test_genomes_loader_qt(tmp_path):
+    """-r: both DBs' lists, query ids offset by nT; F from G restricted to the
+    tetramers present in both DBs (the reference's inner join) is the
+    reference's QT F, and T is its QT T."""
+    t = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    pre = str(tmp_path / "g")
+    r = run(t, str(tmp_path / "o.csv"), "-r", q, "--dump-genomes", pre)
+    assert r.returncode == 0, r.stderr
+    G_off, G_tet = _read_i64_vec(pre + "_g_off.bin"), fm.read_vec_i32(pre + "_g_tet.bin")
+    T = fm.read_matrix_i32(pre + "_t_matrix.bin")
+    assert np.array_equal(T, fm.read_matrix_i32(gpath("xdb_qt_t_matrix.bin")))
+    P, n = T.shape
+    F, _ = _f_from_g(G_off, G_tet, n, P)
+    ref = fm.read_f_array(gpath("xdb_qt_f_array.bin"))
+    # keep the (tetramer, protein) runs holding both a target and a query genome
+    lens = np.diff(G_off)
+    lst = np.repeat(np.arange(n * P, dtype=np.int64), lens)
+    tet = np.sort(G_tet.astype(np.int64) * P + lst % P, kind="stable")  # run key per F entry, F order
+    nT = 4
+    key_t = set(np.unique(tet[F[:, 1] < nT]).tolist())
+    key_q = set(np.unique(tet[F[:, 1] >= nT]).tolist())
+    both = np.array([k in key_t and k in key_q for k in tet])
+    assert np.array_equal(F[both], ref)

@@ -36,7 +36,9 @@ def run(*args):
 def test_cli_csv_bytes(tmp_path, name, devs):
     db = unpack(tmp_path, name + ".db")
     out = tmp_path / "out.csv"
-    run(db, str(out), "--bin", str(tmp_path / "o"), *devs)
+    r = run(db, str(out), "--bin", str(tmp_path / "o"), *devs)
+    # the drop-in runs the benchmarked path: <p>_genomes -> G, F built on the GPU, k_rows_pl
+    assert "<p>_genomes -> G" in r.stdout and "k_rows_pl:" in r.stdout, r.stdout
     assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
     J = fm.read_jac(str(tmp_path / "o_jac.bin"))
     Jr = fm.read_jac(gpath(name + "_jac.bin"))
@@ -115,3 +117,17 @@ def test_cli_stream_aji_qt_ref_compat(tmp_path):
     out = tmp_path / "s_aji.bin"
     run(t, str(tmp_path / "unused.csv"), "-r", q, "--ref-compat", "--stream-aji", str(out), "--tile-pairs", "50")
     assert np.array_equal(fm.read_vec_f64(str(out)), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
+
+
+@pytest.mark.parametrize("loader", ["genomes", "tetras"])
+def test_cli_both_loaders_same_bytes(tmp_path, loader):
+    """--loader tetras (F from `<p>_tetras`, G built on the GPU) and the default
+    G ingest (F built on the GPU) write the same bytes, for -q and -r too."""
+    db = unpack(tmp_path, "xdb_subset1.db")
+    q = unpack(tmp_path, "xdb_subset2.db")
+    r = run(db, str(tmp_path / "a.csv"), "--loader", loader)
+    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert (tmp_path / "a.csv").read_text() == text("xdb_subset1_aji_matrix_wheader.csv")
+    r = run(db, str(tmp_path / "b.csv"), "-r", q, "--loader", loader, "--ref-compat", "--bin", str(tmp_path / "b"))
+    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert np.array_equal(fm.read_vec_f64(str(tmp_path / "b_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))

@@ -1,0 +1,179 @@
+"""BASELINE configs C3, C4 and C5 on the GPU, through the C ABI, against the
+pinned CPU oracle (SURVEY §8d sizes; the reference itself cannot run any of
+them: |E| > 2^31, ds_helper.hpp:209,365; N >= 46 342, ds_impl.hpp:79).
+
+  C3  SYN 10 000 x 100 all-vs-all: kernel |E| == the oracle's exact count,
+      sampled rows bit-exact (S, N, AJI) against the oracle's dense
+      restatement, and the 8-way row-block split of the multi-GPU path
+      (shard.split_rows, one pfaai_run per block on this device) equal to
+      the single run bit for bit.
+  C4  query-vs-target, 50 000 targets x 1 000 queries (the -r path, corrected
+      semantics): |E| == the oracle's count, sampled query rows bit-exact.
+  C5  SYN 100 000 x 100 all-vs-all streamed in output tiles (pfaai_stream):
+      tiles arrive in order and cover every pair, 0 <= AJI <= 1 and
+      1 <= N <= P everywhere, sampled rows and their |E| bit-exact against
+      the oracle.
+
+Each case prints progress to $PFAAI_PROGRESS (if set) so a long GPU call is
+never silent.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+from parfastaai_amd import _capi, syn
+from parfastaai_amd.shard import split_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def progress(msg):
+    path = os.environ.get("PFAAI_PROGRESS")
+    if path:
+        with open(path, "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+def _dev_run(engine, rb, re, n_pairs, flags=0):
+    """pfaai_run of rows [rb, re) into device arrays (full JAC length)."""
+    import torch
+
+    aji = torch.full((n_pairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    S = torch.full((n_pairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    N = torch.full((n_pairs,), -1, dtype=torch.int32, device="cuda:0")
+    engine.run(rb, re, flags | _capi.FLAG_EMIT_JAC, aji.data_ptr(), S.data_ptr(), N.data_ptr(),
+               stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return aji, S, N
+
+
+def _check_all_rows(pr, n, rows, aji, S, N, first=0):
+    """rows of an all-vs-all run (host arrays indexed by JAC index - first)
+    bit-exact against the oracle's dense restatement."""
+    for a in rows:
+        So, No, _ = pr.dense_rows(a, a + 1)
+        b = np.arange(a + 1, n)
+        k = n * a + b - (a + 2) * (a + 1) // 2 - first
+        assert np.array_equal(N[k], No[0, b]), a
+        assert np.array_equal(S[k], So[0, b]), a
+        assert np.array_equal(aji[k], np.where(No[0, b] > 0, So[0, b] / np.maximum(No[0, b], 1), 0.0)), a
+
+
+@pytest.mark.timeout(300)
+def test_c3_10k_all_vs_all_and_8way_rowblocks(engine):
+    n, P = 10000, 100
+    t0 = time.time()
+    g = syn.generate(n, P)
+    pb = dict(mode=_capi.MODE_ALL, n_ids=n, n_prot=P, Lp=g["Lp"], F_prot=g["F_prot"], F_genome=g["F_genome"],
+              T=g["T"], G_off=g["G_off"], G_tet=g["G_tet"])
+    engine.load(**pb)
+    progress(f"C3 generated + loaded in {time.time() - t0:.1f}s")
+    pr = O.Problem(pb)
+    _, npairs = engine.shape()
+    assert npairs == n * (n - 1) // 2
+    aji, S, N = _dev_run(engine, 0, n, npairs)
+    st = engine.stats()
+    assert st["rows_kernel"] == "pl"
+    assert st["n_events"] == pr.count_e()  # the reference's |E| (countTetramerTuples)
+    Ah, Sh, Nh = aji.cpu().numpy(), S.cpu().numpy(), N.cpu().numpy()
+    assert (Nh >= 1).all() and (Nh <= P).all()
+    assert (Ah > 0).all() and (Ah <= 1).all()
+    _check_all_rows(pr, n, [0, 1, 4321, 7777, n - 3], Ah, Sh, Nh)
+    progress("C3 full run checked")
+    # the 8-GPU row-block split, one block per pfaai_run (run table reused)
+    import torch
+
+    a8 = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    S8 = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    N8 = torch.full((npairs,), -1, dtype=torch.int32, device="cuda:0")
+    ev = 0
+    for i, (rb, re) in enumerate(split_rows(n, 8)):
+        f, c = engine.row_span(rb, re)
+        engine.run(rb, re, _capi.FLAG_EMIT_JAC | (_capi.FLAG_KEEP_RUNS if i else 0), a8.data_ptr(), S8.data_ptr(),
+                   N8.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ev += engine.stats()["n_events"]
+    assert ev == st["n_events"]
+    assert torch.equal(a8, aji) and torch.equal(S8, S) and torch.equal(N8, N)
+    progress("C3 8-way row blocks equal")
+
+
+@pytest.mark.timeout(300)
+def test_c4_qt_50000_targets_x_1000_queries(engine):
+    nT, nQ, P, K = 50000, 1000, 100, 20
+    t0 = time.time()
+    gt = syn.generate(nT, P, clade_size=K)
+    gq = syn.generate(nQ, P, clade_size=K, genome_seed=syn.DEFAULT_SEED + 1, n_clades=(nT + K - 1) // K,
+                      clade_mod=True)
+    m = syn.qt_merge(gt, gq)
+    del gt, gq
+    is_q = np.zeros(nT + nQ, np.uint8)
+    is_q[nT:] = 1
+    pb = dict(mode=_capi.MODE_QT, n_ids=nT + nQ, n_prot=P, n_qry=nQ, n_tgt=nT, is_q=is_q, Lp=m["Lp"],
+              F_prot=m["F_prot"], F_genome=m["F_genome"], T=m["T"], G_off=m["G_off"], G_tet=m["G_tet"])
+    engine.load(**pb)
+    progress(f"C4 generated + loaded in {time.time() - t0:.1f}s (|F| = {len(m['F_genome'])})")
+    pr = O.Problem(pb)
+    _, npairs = engine.shape()
+    assert npairs == nQ * nT
+    aji, S, N = _dev_run(engine, 0, nQ, npairs)
+    st = engine.stats()
+    assert st["rows_kernel"] == "pl"
+    assert st["n_events"] == pr.count_e()
+    Ah, Sh, Nh = aji.cpu().numpy(), S.cpu().numpy(), N.cpu().numpy()
+    assert (Nh >= 0).all() and (Nh <= P).all() and (Ah >= 0).all() and (Ah <= 1).all()
+    for q in (0, 1, 499, nQ - 1):
+        So, No, _ = pr.dense_rows(nT + q, nT + q + 1)
+        k = slice(q * nT, (q + 1) * nT)
+        assert np.array_equal(Nh[k], No[0, :nT]), q
+        assert np.array_equal(Sh[k], So[0, :nT]), q
+        assert np.array_equal(Ah[k], np.where(No[0, :nT] > 0, So[0, :nT] / np.maximum(No[0, :nT], 1), 0.0)), q
+    progress("C4 checked")
+
+
+@pytest.mark.timeout(600)
+def test_c5_100k_streamed_tiles(engine):
+    n, P = 100000, 100
+    t0 = time.time()
+    g = syn.generate(n, P)
+    pb = dict(mode=_capi.MODE_ALL, n_ids=n, n_prot=P, Lp=g["Lp"], F_prot=g["F_prot"], F_genome=g["F_genome"],
+              T=g["T"], G_off=g["G_off"], G_tet=g["G_tet"])
+    progress(f"C5 generated in {time.time() - t0:.1f}s (|F| = {len(g['F_genome'])})")
+    engine.load(**pb)
+    progress(f"C5 loaded at {time.time() - t0:.1f}s")
+    pr = O.Problem(pb)
+    n_rows, npairs = engine.shape()
+    sample = [0, 1, 31337, 77777, n - 2]
+    got = {}
+    seen = []
+    bad = []
+
+    def sink(rb, re, first, a, s, nn):
+        if seen and seen[-1][1] != rb:
+            bad.append(("order", rb))
+        seen.append((rb, re, first, len(a)))
+        if not ((a > 0) & (a <= 1)).all() or not ((nn >= 1) & (nn <= P)).all():
+            bad.append(("range", rb))
+        for r in sample:
+            if rb <= r < re:
+                f, c = engine.row_span(r, r + 1)
+                got[r] = (a[f - first: f - first + c].copy(), s[f - first: f - first + c].copy(),
+                          nn[f - first: f - first + c].copy())
+        if len(seen) % 4 == 0:
+            progress(f"C5 tile {len(seen)} rows [{rb}, {re})")
+        return 0
+
+    ne = engine.stream(0, n_rows, 1 << 28, _capi.FLAG_EMIT_JAC, sink)
+    progress(f"C5 streamed {len(seen)} tiles at {time.time() - t0:.1f}s")
+    assert not bad, bad[:5]
+    assert seen[0][0] == 0 and seen[-1][1] == n_rows and len(seen) > 1
+    assert sum(x[3] for x in seen) == npairs
+    assert ne == pr.count_e()  # |E| over all 5e9 pairs = the reference's count
+    for r in sample:
+        a, s, nn = got[r]
+        f, _ = engine.row_span(r, r + 1)
+        _check_all_rows(pr, n, [r], a, s, nn, first=f)
+    progress("C5 checked")

@@ -44,3 +44,36 @@ def test_load_rejects_bad_input(engine, n, P):
     engine.load(**pb)  # the good problem still loads and runs
     aji, _, _ = engine.compute(0)
     assert len(aji) == n * (n - 1) // 2 and np.all((aji >= 0) & (aji <= 1))
+
+
+@pytest.mark.parametrize("n,P", [(60, 8), (400, 100)], ids=["small", "threaded"])
+def test_load_rejects_bad_lp_and_g(engine, n, P):
+    """Lp is checked (non-decreasing, so every interior entry <= n_f) before
+    any F access; G lists must be strictly ascending sets of F's
+    memberships (checked on the device against F)."""
+    pb = _pb(n, P)
+    nf = len(pb["F_genome"])
+    cases = []
+    b = dict(pb); b["Lp"] = pb["Lp"].copy(); b["Lp"][5] = nf + 1000  # interior past the end
+    cases.append((b, "non-decreasing"))
+    b = dict(pb); b["Lp"] = pb["Lp"].copy()
+    t = int(np.flatnonzero(np.diff(b["Lp"]) > 0)[len(b["Lp"]) // 4 % 7])
+    b["Lp"][t + 1], b["Lp"][t] = b["Lp"][t], b["Lp"][t + 1] + 1  # a descent
+    cases.append((b, "non-decreasing"))
+    G_off, G_tet = pb["G_off"], pb["G_tet"]
+    k = int(np.flatnonzero(np.diff(G_off) >= 3)[-1])
+    lo = int(G_off[k])
+    b = dict(pb); b["G_tet"] = G_tet.copy(); b["G_tet"][[lo, lo + 1]] = b["G_tet"][[lo + 1, lo]]
+    cases.append((b, "strictly ascending"))
+    # a membership F does not hold: the last entry of a list moved to a free tetramer above it
+    hi = int(G_off[k + 1]) - 1
+    if G_tet[hi] + 1 < 160000:
+        b = dict(pb); b["G_tet"] = G_tet.copy(); b["G_tet"][hi] += 1
+        cases.append((b, "does not hold"))
+    for bad, what in cases:
+        with pytest.raises(_capi.PfaaiError) as ei:
+            engine.load(**bad)
+        assert ei.value.code == 7 and what in str(ei.value), (what, str(ei.value))
+    engine.load(**pb)
+    aji, _, _ = engine.compute(0)
+    assert np.all((aji > 0) & (aji <= 1))

@@ -1,6 +1,9 @@
 """Build recipes for the native pieces (no cmake, no pip).
 
   hip      parfastaai_amd/lib/libpfaai_hip.so   hipcc --offload-arch=gfx950
+  diag     parfastaai_amd/lib/libpfaai_hip_diag.so  the same with -DPFAAI_DIAGNOSTICS
+                                                (ablation / stage-clock switches;
+                                                built only on request: --diag)
   cli      parfastaai_amd/lib/par_fastaai_amd   g++ host CLI over the C ABI
   syn      tools/_build/libpfaai_syn.so         synthetic DB generator
   oracle   oracle/_build/libpfaai_oracle.so     CPU oracle (test infra)
@@ -33,16 +36,16 @@ def _newer(out, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def build_hip(force=False):
+def build_hip(force=False, diag=False):
     src = os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_hip.hip")
     csrc = os.path.join(ROOT, "parfastaai_amd/csrc")
     deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include/pfaai_hip.h")]
-    out = os.path.join(ROOT, "parfastaai_amd/lib/libpfaai_hip.so")
+    out = os.path.join(ROOT, "parfastaai_amd/lib", "libpfaai_hip_diag.so" if diag else "libpfaai_hip.so")
     if force or _newer(out, deps):
         os.makedirs(os.path.dirname(out), exist_ok=True)
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
               "-ffp-contract=off", "-fno-fast-math", "-Wall", "-I" + os.path.join(ROOT, "include"),
-              "-o", out, src])
+              *(["-DPFAAI_DIAGNOSTICS"] if diag else []), "-o", out, src])
     return out
 
 
@@ -98,3 +101,5 @@ def build_all(force=False):
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
+    if "--diag" in sys.argv:
+        build_hip(force="--force" in sys.argv, diag=True)

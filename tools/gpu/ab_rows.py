@@ -1,7 +1,8 @@
 """Interleaved A/B of k_rows variants in one process (SYN all-vs-all).
 
     python tools/gpu/ab_rows.py --genomes 10000 --rounds 5 --variants PFAAI_ROWS_KERNEL=pl PFAAI_ROWS_KERNEL=fused
-Each variant is an env setting read by pfaai_run (PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist, PFAAI_ABLATE).
+Each variant is an env setting read by pfaai_run (PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist; PFAAI_ABLATE only
+with the diagnostics library: PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so).
 Prints per-variant median/min of build and row-kernel device times.
 """
 import argparse

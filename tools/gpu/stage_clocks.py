@@ -1,6 +1,10 @@
-"""k_rows_pl stage clocks at 10k (PFAAI_PL_CLK=1): where the protein loop's
+"""k_rows_pl stage clocks at 10k (PFAAI_PL_CLK=1, diagnostics library:
+`python tools/build_native.py --diag`, loaded through PFAAI_HIP_LIB): where the protein loop's
 time goes, per stage, for the waves of the first 256 workgroups."""
 import os
+
+os.environ.setdefault("PFAAI_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "parfastaai_amd", "lib", "libpfaai_hip_diag.so"))
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
