@@ -62,10 +62,11 @@ enum { PFAAI_MODE_ALL = 0, PFAAI_MODE_QSUB = 1, PFAAI_MODE_QT = 2 };
                                     load built (same stream or ordered after it):
                                     row tiles / pipelined shards pay k_blk once */
 
-/* Row kernels (pfaai_run_info): k_rows_pl (genome-major walk, the default),
- * its 512-thread form, the fused k_rows (G lists > 1024 entries), and the
- * work-list k_rows (no genome-major view could be formed). */
-enum { PFAAI_ROWS_PL = 0, PFAAI_ROWS_PL512 = 1, PFAAI_ROWS_FUSED = 2, PFAAI_ROWS_WORKLIST = 3 };
+/* Row kernels (pfaai_run_info): k_rows_pl (genome-major walk), its 512-
+ * thread form, the fused k_rows (G lists > 1024 entries), the work-list
+ * k_rows (no genome-major view could be formed), and k_rows_v2 (wave-local
+ * line tasks, every load one protein ahead). */
+enum { PFAAI_ROWS_PL = 0, PFAAI_ROWS_PL512 = 1, PFAAI_ROWS_FUSED = 2, PFAAI_ROWS_WORKLIST = 3, PFAAI_ROWS_V2 = 4 };
 
 typedef struct pfaai_ctx pfaai_ctx;
 
@@ -104,9 +105,10 @@ typedef struct {
      * builds it on the device from F (stable radix sort of the F entries by
      * genome * n_prot + protein), so F-only callers -- the reference's own
      * DataStructInterface classes -- run the same kernels.  When both F and
-     * G are given, G must list exactly the memberships of F (checked on the
-     * device: every G entry's genome is found in its run of F, |G| == |F|,
-     * lists strictly ascending). */
+     * G are given, G must hold every membership of F, and may hold more only
+     * where F has no run (t, p) at all -- the -r case: both DBs' lists vs
+     * the inner-joined F (checked on the device).  Lists are strictly
+     * ascending sets of tetramer ids. */
     const int64_t* G_off;  /* [n_ids * n_prot + 1] */
     const int32_t* G_tet;  /* [G_off[n_ids * n_prot]] */
 } pfaai_problem;

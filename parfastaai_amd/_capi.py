@@ -35,7 +35,7 @@ EXPORTS = [
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
     "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info",
 ]
-ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist"}
+ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
 #          const double* S, const int32_t* N)   (pfaai_sink_fn)

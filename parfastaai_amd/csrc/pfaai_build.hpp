@@ -16,7 +16,7 @@
 //              (tetramer, protein) run in ascending genome order -- exactly
 //              the reference's F (the UNION ALL ... ORDER BY of
 //              scp_db.hpp:161-216).  Lc is counted on the way in.
-// When both are given, k_g_check proves they list the same memberships.
+// When both are given, k_g_check proves that G covers F.
 #pragma once
 #include "pfaai_kernels.hpp"
 
@@ -66,15 +66,18 @@ __global__ void k_fp16(const int32_t* __restrict__ Fp, int64_t n, uint16_t* __re
         Fp16[i] = (uint16_t)Fp[i];
 }
 
-// Both F and G given: every G entry (genome g, protein p, tetramer t) must
-// be a member of F's run (t, p) -- binary search for (p, g) in F's
-// tetramer block, which is sorted by (protein, genome).  With |G| == |F|
-// and strictly ascending lists (host-checked) G and F then hold the same
-// memberships.  One wave per list.
+// Both F and G given: G must hold every membership of F, and an entry
+// (genome g, protein p, tetramer t) of G that is not in F is allowed only
+// where F has no run (t, p) at all (e.g. the -r path: G holds every tetramer
+// of both DBs, F only those in both, scp_db.hpp:459-466; such an entry meets
+// an empty run in the row kernels).  Binary search for (p, g) in F's
+// tetramer block, sorted by (protein, genome); *found counts the entries F
+// holds (== |F| when G covers F, lists being strictly ascending sets).  One
+// wave per list.
 __global__ __launch_bounds__(256) void k_g_check(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                  const int32_t* __restrict__ Fg, const int64_t* __restrict__ G_off,
                                                  const int32_t* __restrict__ G_tet, int64_t n_lists, int32_t P,
-                                                 int* __restrict__ err) {
+                                                 int* __restrict__ err, unsigned long long* __restrict__ found) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t L = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); L < n_lists; L += waves) {
@@ -82,18 +85,26 @@ __global__ __launch_bounds__(256) void k_g_check(const int64_t* __restrict__ Lp,
         const uint64_t key = ((uint64_t)(uint32_t)p << 32) | (uint32_t)g;
         const int64_t e = G_off[L + 1];
         bool bad = false;
+        uint32_t hit = 0;
         for (int64_t k = G_off[L] + lane; k < e; k += 64) {
             const int32_t t = G_tet[k];
-            int64_t lo = Lp[t], hi = Lp[t + 1];
-            const int64_t end = hi;
+            const int64_t start = Lp[t], end = Lp[t + 1];
+            int64_t lo = start, hi = end;
             while (lo < hi) {
                 const int64_t mid = (lo + hi) >> 1;
                 const uint64_t m = ((uint64_t)(uint32_t)Fp[mid] << 32) | (uint32_t)Fg[mid];
                 if (m < key) lo = mid + 1; else hi = mid;
             }
-            bad |= lo >= end || Fp[lo] != p || Fg[lo] != g;
+            const bool in_run = lo < end && Fp[lo] == p;
+            if (in_run && Fg[lo] == g) {
+                ++hit;
+            } else {  // not a member: only allowed where F has no run (t, p)
+                bad |= in_run || (lo > start && Fp[lo - 1] == p);
+            }
         }
         if (bad) atomicOr(err, 1);
+        hit = wave_sum_u32_fwd(hit);
+        if (lane == 0 && hit) atomicAdd(found, (unsigned long long)hit);
     }
 }
 

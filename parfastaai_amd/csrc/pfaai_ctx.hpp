@@ -1,0 +1,194 @@
+// pfaai_ctx.hpp -- the engine context (pfaai_ctx) and the host helpers
+// shared by the C-ABI translation unit (pfaai_hip.hip) and the row-kernel
+// translation units (pfaai_rows_m{0,1,2}.hip, one per mode, compiled in
+// parallel: each instantiates launch_rows<MODE> of pfaai_launch.hpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <system_error>
+#include <thread>
+#include <vector>
+
+#include "pfaai_hip.h"
+#include "pfaai_kernels.hpp"
+#include "pfaai_rows_v2.hpp"  // kernel constants (kPlEntries, kV2Threads, kClkBlocks); templates only
+
+// Diagnostic switches that change results or instrument the kernels
+// (PFAAI_ABLATE, PFAAI_BLK_ABLATE: skip kernel phases; PFAAI_PL_CLK: stage
+// clocks; PFAAI_DIV_NEWTON: the division self-test's refinement count) exist
+// only in a library built with -DPFAAI_DIAGNOSTICS (tools/build_native.py
+// --diag -> libpfaai_hip_diag.so).  The release library never reads them.
+#ifdef PFAAI_DIAGNOSTICS
+#define DIAG_ENV(name) getenv(name)
+#else
+#define DIAG_ENV(name) (static_cast<const char*>(nullptr))
+#endif
+
+namespace pfaai_impl {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace pfaai_impl
+
+struct pfaai_ctx {
+    using DevBuf = pfaai_impl::DevBuf;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool loaded = false;
+
+    // problem (host copies of scalars + small maps)
+    pfaai_problem prob{};
+    int64_t n_rows = 0, n_pairs = 0;
+    std::vector<int32_t> row_genome_h;
+    std::vector<int32_t> q_index_h;
+    int32_t max_cols = 0;
+
+    // device-resident problem
+    DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
+    int64_t max_glen = 0;  // longest (genome, protein) G list
+    DevBuf Fp16;
+    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
+    bool has_g = false;
+    bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
+    bool runs_key = false;
+    bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
+    pfaai::Dev dev{};
+
+    // work space (sized at load for all rows, so runs never allocate)
+    DevBuf cnt_t, off_t;
+    DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
+    DevBuf out_aji, out_S, out_N, dbg;
+    std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
+
+    // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t st_done[2] = {nullptr, nullptr}, st_copied[2] = {nullptr, nullptr};
+    void* st_host = nullptr;
+    size_t st_host_bytes = 0;
+    DevBuf st_dev;
+    int64_t st_events = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    bool timed = false;
+    int rows_kernel = 0;  // RowsKernel of the current run
+    // per-run event triples for pfaai_timing (pool reused after each reset)
+    std::vector<hipEvent_t> pool;
+    size_t pool_used = 0;
+    bool windows = false;  // this run: absolute column windows, a run table per window
+    DevBuf blkw;           // the window tables (window-major), built by k_blk<true>
+    bool win_valid = false, win_key = false;
+    int64_t win_cols = 0;
+    // the next (start, after build, after rows) event triple of the pool
+    hipEvent_t* take_events() {
+        while (pool.size() < pool_used + 3) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        hipEvent_t* ev = &pool[pool_used];
+        pool_used += 3;
+        ev0 = ev[0];
+        ev1 = ev[1];
+        ev2 = ev[2];
+        return ev;
+    }
+};
+
+namespace pfaai_impl {
+
+using namespace pfaai;
+
+// Row kernels.  PL (k_rows_pl, 1024 threads, <= 64 VGPRs so two workgroups
+// share a CU: 12.2 ms at 10k vs 15.6 at one per CU) is the default for
+// genome-major input; PL512 is its 512-thread form (13.9 ms); FUSED (k_rows<true>) takes
+// G lists longer than k_rows_pl does; WORKLIST (k_rows<false> over sorted
+// work lists) serves F-only input.  PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist
+// overrides the choice (A/B runs, tools/gpu/ab_rows.py; tests).
+constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
+
+enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3, RK_V2 = 4 };
+
+// scalars buffer layout (u64 each)
+enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
+
+inline int fail(pfaai_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+inline int hip_fail(pfaai_ctx* c, hipError_t e, const char* what) {
+    if (e == hipErrorOutOfMemory)
+        return fail(c, PFAAI_RC_OOM, std::string(what) + ": " + hipGetErrorString(e));
+    return fail(c, PFAAI_RC_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, call)                                  \
+    do {                                                   \
+        hipError_t e_ = (call);                            \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+    } while (0)
+
+inline int ensure(pfaai_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return PFAAI_RC_OK;
+    if (b.p) {
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    if (bytes == 0) bytes = 8;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc");
+    b.bytes = bytes;
+    return PFAAI_RC_OK;
+}
+
+inline void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+template <typename T>
+inline int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
+    int rc = ensure(c, b, n * sizeof(T));
+    if (rc) return rc;
+    if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return PFAAI_RC_OK;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Counter words per thread: the smallest KW with KW * nt >= the widest row
+// (in u16 pairs); wider rows are cut into column chunks of 2 * KW * nt.
+template <int NT>
+inline int pick_kw(int32_t max_cols, int kw_max) {
+    const int64_t words = ceil_div((int64_t)std::max<int32_t>(max_cols, 1) + 1, 2);
+    for (int kw = 1; kw < kw_max; ++kw)
+        if (words <= (int64_t)kw * NT) return kw;
+    return kw_max;
+}
+
+// k_rows_pl's chunk width for this problem (launch_rows' KW choice)
+inline int64_t pl_chunk_cols(pfaai_ctx* c) {
+    if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->max_cols, 10);
+    if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->max_cols, 5);
+    const char* km = getenv("PFAAI_PL_KWMAX");
+    return 2 * 1024 * (int64_t)pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+}
+
+// Row kernels for output rows [rb, re) (pfaai_launch.hpp; instantiated per
+// mode in pfaai_rows_m{0,1,2}.hip).
+template <int MODE>
+void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                 hipStream_t s);
+
+}  // namespace pfaai_impl

@@ -4,7 +4,6 @@
 // resident in HBM after pfaai_load(); pfaai_run() is stream-ordered device
 // work only (no host sync, no allocation): the run table (k_blk) or, for
 // F-only input, the sorted work lists, then the row kernel (K-S+J).
-#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
@@ -17,156 +16,15 @@
 #include <vector>
 
 #include "pfaai_hip.h"
+#include "pfaai_aux.hpp"
 #include "pfaai_build.hpp"
-#include "pfaai_kernels.hpp"
-#include "pfaai_rows_pl.hpp"
+#include "pfaai_ctx.hpp"
 
 using namespace pfaai;
 
-// Diagnostic switches that change results or instrument the kernels
-// (PFAAI_ABLATE, PFAAI_BLK_ABLATE: skip kernel phases; PFAAI_PL_CLK: stage
-// clocks; PFAAI_DIV_NEWTON: the division self-test's refinement count) exist
-// only in a library built with -DPFAAI_DIAGNOSTICS (tools/build_native.py
-// --diag -> libpfaai_hip_diag.so).  The release library never reads them.
-#ifdef PFAAI_DIAGNOSTICS
-#define DIAG_ENV(name) getenv(name)
-#else
-#define DIAG_ENV(name) (static_cast<const char*>(nullptr))
-#endif
+using namespace pfaai_impl;
 
 namespace {
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-};
-
-}  // namespace
-
-struct pfaai_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-    bool loaded = false;
-
-    // problem (host copies of scalars + small maps)
-    pfaai_problem prob{};
-    int64_t n_rows = 0, n_pairs = 0;
-    std::vector<int32_t> row_genome_h;
-    std::vector<int32_t> q_index_h;
-    int32_t max_cols = 0;
-
-    // device-resident problem
-    DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
-    int64_t max_glen = 0;  // longest (genome, protein) G list
-    DevBuf Fp16;
-    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
-    bool has_g = false;
-    bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
-    bool runs_key = false;
-    bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
-    Dev dev{};
-
-    // work space (sized at load for all rows, so runs never allocate)
-    DevBuf cnt_t, off_t;
-    DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
-    DevBuf out_aji, out_S, out_N, dbg;
-    std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
-
-    // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
-    hipStream_t copy_stream = nullptr;
-    hipEvent_t st_done[2] = {nullptr, nullptr}, st_copied[2] = {nullptr, nullptr};
-    void* st_host = nullptr;
-    size_t st_host_bytes = 0;
-    DevBuf st_dev;
-    int64_t st_events = 0;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-    bool timed = false;
-    int rows_kernel = 0;  // RowsKernel of the current run
-    // per-run event triples for pfaai_timing (pool reused after each reset)
-    std::vector<hipEvent_t> pool;
-    size_t pool_used = 0;
-    bool windows = false;  // this run: absolute column windows, a run table per window
-    DevBuf blkw;           // the window tables (window-major), built by k_blk<true>
-    bool win_valid = false, win_key = false;
-    int64_t win_cols = 0;
-    // the next (start, after build, after rows) event triple of the pool
-    hipEvent_t* take_events() {
-        while (pool.size() < pool_used + 3) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
-            pool.push_back(e);
-        }
-        hipEvent_t* ev = &pool[pool_used];
-        pool_used += 3;
-        ev0 = ev[0];
-        ev1 = ev[1];
-        ev2 = ev[2];
-        return ev;
-    }
-};
-
-namespace {
-
-// Row kernels.  PL (k_rows_pl, 1024 threads, <= 64 VGPRs so two workgroups
-// share a CU: 12.2 ms at 10k vs 15.6 at one per CU) is the default for
-// genome-major input; PL512 is its 512-thread form (13.9 ms); FUSED (k_rows<true>) takes
-// G lists longer than k_rows_pl does; WORKLIST (k_rows<false> over sorted
-// work lists) serves F-only input.  PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist
-// overrides the choice (A/B runs, tools/gpu/ab_rows.py; tests).
-constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
-
-enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
-
-// scalars buffer layout (u64 each)
-enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_N = 5 };
-
-int fail(pfaai_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
-    return code;
-}
-
-int hip_fail(pfaai_ctx* c, hipError_t e, const char* what) {
-    if (e == hipErrorOutOfMemory)
-        return fail(c, PFAAI_RC_OOM, std::string(what) + ": " + hipGetErrorString(e));
-    return fail(c, PFAAI_RC_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-#define HIPCHK(ctx, call)                                  \
-    do {                                                   \
-        hipError_t e_ = (call);                            \
-        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
-    } while (0)
-
-int ensure(pfaai_ctx* c, DevBuf& b, size_t bytes) {
-    if (b.bytes >= bytes && b.p) return PFAAI_RC_OK;
-    if (b.p) {
-        (void)hipFree(b.p);
-        b.p = nullptr;
-        b.bytes = 0;
-    }
-    if (bytes == 0) bytes = 8;
-    hipError_t e = hipMalloc(&b.p, bytes);
-    if (e != hipSuccess) return hip_fail(c, e, "hipMalloc");
-    b.bytes = bytes;
-    return PFAAI_RC_OK;
-}
-
-void release(DevBuf& b) {
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.bytes = 0;
-}
-
-template <typename T>
-int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
-    int rc = ensure(c, b, n * sizeof(T));
-    if (rc) return rc;
-    if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
-    return PFAAI_RC_OK;
-}
-
-int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Host-side checks of pfaai_load over |F|-sized arrays: [0, n) split over up
 // to 16 threads, one per 2^20 units of `work` (default n): fn(lo, hi, thread).
@@ -329,135 +187,6 @@ int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* ou
     return PFAAI_RC_OK;
 }
 
-// Counter words per thread: the smallest KW with KW * nt >= the widest row
-// (in u16 pairs); wider rows are cut into column chunks of 2 * KW * nt.
-template <int NT>
-int pick_kw(int32_t max_cols, int kw_max) {
-    const int64_t words = ceil_div((int64_t)std::max<int32_t>(max_cols, 1) + 1, 2);
-    for (int kw = 1; kw < kw_max; ++kw)
-        if (words <= (int64_t)kw * NT) return kw;
-    return kw_max;
-}
-
-// k_rows_pl's chunk width for this problem (launch_rows' KW choice)
-int64_t pl_chunk_cols(pfaai_ctx* c) {
-    if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->max_cols, 10);
-    const char* km = getenv("PFAAI_PL_KWMAX");
-    return 2 * 1024 * (int64_t)pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
-}
-
-template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
-void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-               hipStream_t s) {
-    const int32_t chunk = 2 * KW * NT;
-    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
-    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
-    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
-    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
-        if (bigf)
-            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, true>), dim3(r1 - r0, gy), dim3(NT), lds, s,
-                               dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-        else
-            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv,
-                               r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    };
-    if (nchunks == 1 || !c->windows) {
-        rows(c->dev, rb, re, nchunks, -1);
-        return;
-    }
-    // rows wider than one chunk (c->windows, set by run_mode, which built the
-    // window tables): per absolute column window, the rows with columns in it
-    // over that window's table
-    const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
-    const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
-    for (int32_t w = 0; w < nwin; ++w) {
-        int64_t r1 = re;
-        if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
-        if (r1 <= rb) continue;
-        Dev dw = c->dev;
-        dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
-        rows(dw, rb, r1, 1, w);
-    }
-}
-
-template <int MODE, int KW>
-void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-                   hipStream_t s) {
-    const int32_t chunk = 2 * KW * kRowThreads;
-    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
-    const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
-    auto* recs = static_cast<const uint2*>(c->recs.p);
-    if (c->rows_kernel == RK_FUSED)
-        hipLaunchKernelGGL((k_rows<MODE, KW, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else
-        hipLaunchKernelGGL((k_rows<MODE, KW, false>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
-                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-}
-
-template <int MODE>
-void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-                 hipStream_t s) {
-#define PL_CASE(NT, K) \
-    case K: launch_pl<MODE, K, NT>(c, rb, re, flags, aji, S, N, s); break;
-#define KR_CASE(K) \
-    case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
-    if (c->rows_kernel == RK_PL) {
-        const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
-        const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
-#ifdef PFAAI_DIAGNOSTICS
-        if (MODE == 0 && kw == 5 && !c->windows && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
-            const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
-            const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
-            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
-            auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
-                               chunk, -1, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
-                               static_cast<unsigned long long*>(c->dbg.p));
-            return;
-        }
-#endif
-        // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
-        const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
-        if (nl) {
-            switch (kw) {
-                case 1: launch_pl<MODE, 1, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 2: launch_pl<MODE, 2, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 3: launch_pl<MODE, 3, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 4: launch_pl<MODE, 4, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                default: launch_pl<MODE, 5, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-            }
-            return;
-        }
-        switch (kw) {
-            case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 4: launch_pl<MODE, 4, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            default: launch_pl<MODE, 5, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-        }
-    } else if (c->rows_kernel == RK_PL512) {
-        switch (pick_kw<512>(c->max_cols, 10)) {
-            PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
-            PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
-            default: break;
-        }
-    } else {
-        switch (pick_kw<kRowThreads>(c->max_cols, 10)) {
-            KR_CASE(1) KR_CASE(2) KR_CASE(3) KR_CASE(4) KR_CASE(5) KR_CASE(6) KR_CASE(8) KR_CASE(10)
-            case 7: launch_k_rows<MODE, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 9: launch_k_rows<MODE, 10>(c, rb, re, flags, aji, S, N, s); break;
-            default: break;
-        }
-    }
-#undef PL_CASE
-#undef KR_CASE
-}
-
 // Work-list space for the sorted (F-only) path, sized for all rows: ~36 B per
 // F entry of the row genomes.  The genome-major kernels need none of it, so
 // it is allocated at load only for F-only input (and on first use by
@@ -504,7 +233,8 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     const int64_t wcols = pl_chunk_cols(c);
     {
         const char* wv = getenv("PFAAI_PL_WINDOWS");
-        c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && !(wv && wv[0] == '0') &&
+        c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
+                     !(wv && wv[0] == '0') &&
                      (int64_t)c->max_cols + 1 > wcols;
         if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 64 KB of LDS
             nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
@@ -747,7 +477,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
             return fail(c, PFAAI_RC_INVALID, "Lp must start at 0 and end at n_f");
         for (int t = 0; t < PFAAI_NTETRAMERS; ++t)
             if (p.Lp[t + 1] < p.Lp[t]) return fail(c, PFAAI_RC_INVALID, "Lp must be non-decreasing");
-        if (in_g && n_g != n_f) return fail(c, PFAAI_RC_INVALID, "G must list exactly F's memberships (|G| != |F|)");
+        if (in_g && n_g < n_f) return fail(c, PFAAI_RC_INVALID, "G must hold every membership of F (|G| < |F|)");
         std::vector<std::vector<int64_t>> fc(16);
         std::atomic<int> bad_id{0}, bad_p{0}, bad_sort{0};
         const int nth = par_for(p.n_f, [&](int64_t lo, int64_t hi, int t) {
@@ -893,19 +623,23 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         return rc;
     }
     bool has_g = in_g;
-    if (in_g && in_f && n_f) {  // both given: G must list F's memberships
+    if (in_g && in_f && n_f) {  // both given: G must hold F's memberships (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
         int* err = reinterpret_cast<int*>(sc + SC_ERR);
         HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
+        HIPCHK(c, hipMemsetAsync(sc + SC_GRAND, 0, sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_g_check, dim3((int)std::min<int64_t>(ceil_div(ng, 4), 1 << 16)), dim3(256), 0, s,
                            static_cast<const int64_t*>(c->Lp.p), static_cast<const int32_t*>(c->Fp.p),
                            static_cast<const int32_t*>(c->Fg.p), static_cast<const int64_t*>(c->G_off.p),
-                           static_cast<const int32_t*>(c->G_tet.p), ng, P, err);
+                           static_cast<const int32_t*>(c->G_tet.p), ng, P, err, sc + SC_GRAND);
         HIPCHK(c, hipGetLastError());
         int bad = 0;
+        unsigned long long found = 0;
         HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(&found, sc + SC_GRAND, sizeof(found), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         if (bad) return fail(c, PFAAI_RC_INVALID, "G lists a membership that F does not hold");
+        if ((int64_t)found != n_f) return fail(c, PFAAI_RC_INVALID, "G does not hold every membership of F");
     } else if (!in_g && ng < ((int64_t)1 << 32)) {  // G from F (keys g * P + p fit 32 bits)
         if ((rc = build_g_from_f(c, ng, n_f, s))) return rc;
         std::vector<int64_t> goff(ng + 1);
@@ -1068,15 +802,16 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         if (const char* v = getenv("PFAAI_ROWS_KERNEL")) {
             const std::string x(v);
             if (x == "pl") k = RK_PL;
+            else if (x == "v2") k = RK_V2;
             else if (x == "pl512") k = RK_PL512;
             else if (x == "fused") k = RK_FUSED;
             else if (x == "worklist") k = RK_WORKLIST;
-            else return fail(c, PFAAI_RC_INVALID, "PFAAI_ROWS_KERNEL must be pl, pl512, fused or worklist");
+            else return fail(c, PFAAI_RC_INVALID, "PFAAI_ROWS_KERNEL must be pl, v2, pl512, fused or worklist");
         }
         if (!c->has_g && k != RK_WORKLIST) k = RK_WORKLIST;       // the others walk the G lists
         if (c->max_glen > kPlEntries && k != RK_WORKLIST) k = RK_FUSED;  // lists too long
         // k_rows_pl addresses the run table with 32-bit buffer offsets
-        if ((uint64_t)c->prob.n_prot * PFAAI_NTETRAMERS * 16u >= (1ull << 32) && (k == RK_PL || k == RK_PL512))
+        if ((uint64_t)c->prob.n_prot * PFAAI_NTETRAMERS * 16u >= (1ull << 32) && (k == RK_PL || k == RK_PL512 || k == RK_V2))
             k = RK_FUSED;
         c->rows_kernel = k;
     }

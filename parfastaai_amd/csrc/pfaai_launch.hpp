@@ -1,0 +1,182 @@
+// pfaai_launch.hpp -- launchers of the row kernels (k_rows_pl, k_rows_v2,
+// k_rows): kernel variant, counter words per thread, column chunks and
+// column windows.  Included by the per-mode translation units
+// pfaai_rows_m{0,1,2}.hip only.
+#pragma once
+#include "pfaai_ctx.hpp"
+#include "pfaai_rows_pl.hpp"
+#include "pfaai_rows_v2.hpp"
+
+namespace pfaai_impl {
+
+template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
+void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+               hipStream_t s) {
+    const int32_t chunk = 2 * KW * NT;
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
+    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    // S5 first in the protein loop (k_rows_pl S5F); PFAAI_PL_S5F=0 for the old order (A/B)
+    const char* s5e = getenv("PFAAI_PL_S5F");
+    const bool s5f = !(s5e && s5e[0] == '0');
+    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
+#define PLK(BF, SF)                                                                                                  \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, BF, SF>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, \
+                       chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+        if (bigf) {
+            if (s5f) PLK(true, true); else PLK(true, false);
+        } else {
+            if (s5f) PLK(false, true); else PLK(false, false);
+        }
+#undef PLK
+    };
+    if (nchunks == 1 || !c->windows) {
+        rows(c->dev, rb, re, nchunks, -1);
+        return;
+    }
+    // rows wider than one chunk (c->windows, set by run_mode, which built the
+    // window tables): per absolute column window, the rows with columns in it
+    // over that window's table
+    const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
+    const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
+    for (int32_t w = 0; w < nwin; ++w) {
+        int64_t r1 = re;
+        if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
+        if (r1 <= rb) continue;
+        Dev dw = c->dev;
+        dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
+        rows(dw, rb, r1, 1, w);
+    }
+}
+
+// k_rows_v2 (pfaai_rows_v2.hpp): one 1024-thread workgroup per CU, same
+// chunk and column-window rules as launch_pl
+template <int MODE, int KW>
+void launch_v2(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+               hipStream_t s) {
+    const int32_t chunk = 2 * KW * kV2Threads;
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const size_t lds = (4 * (size_t)KW * kV2Threads + c->prob.n_prot + 1) * sizeof(uint32_t);  // u32 counters x 2
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
+#ifdef PFAAI_DIAGNOSTICS
+        if (KW == 5 && !bigf && DIAG_ENV("PFAAI_V2_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+            hipLaunchKernelGGL((k_rows_v2<MODE, KW, false, true>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0,
+                               chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
+                               static_cast<unsigned long long*>(c->dbg.p));
+            return;
+        }
+#endif
+        if (bigf)
+            hipLaunchKernelGGL((k_rows_v2<MODE, KW, true>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0, chunk,
+                               abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+        else
+            hipLaunchKernelGGL((k_rows_v2<MODE, KW, false>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0,
+                               chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    };
+    if (nchunks == 1 || !c->windows) {
+        rows(c->dev, rb, re, nchunks, -1);
+        return;
+    }
+    const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
+    const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
+    for (int32_t w = 0; w < nwin; ++w) {
+        int64_t r1 = re;
+        if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
+        if (r1 <= rb) continue;
+        Dev dw = c->dev;
+        dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
+        rows(dw, rb, r1, 1, w);
+    }
+}
+
+template <int MODE, int KW>
+void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                   hipStream_t s) {
+    const int32_t chunk = 2 * KW * kRowThreads;
+    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
+    const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
+    auto* recs = static_cast<const uint2*>(c->recs.p);
+    if (c->rows_kernel == RK_FUSED)
+        hipLaunchKernelGGL((k_rows<MODE, KW, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+    else
+        hipLaunchKernelGGL((k_rows<MODE, KW, false>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
+                           rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
+}
+
+template <int MODE>
+void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                 hipStream_t s) {
+#define PL_CASE(NT, K) \
+    case K: launch_pl<MODE, K, NT>(c, rb, re, flags, aji, S, N, s); break;
+#define KR_CASE(K) \
+    case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
+    if (c->rows_kernel == RK_V2) {
+        switch (pick_kw<kV2Threads>(c->max_cols, 5)) {
+            case 1: launch_v2<MODE, 1>(c, rb, re, flags, aji, S, N, s); break;
+            case 2: launch_v2<MODE, 2>(c, rb, re, flags, aji, S, N, s); break;
+            case 3: launch_v2<MODE, 3>(c, rb, re, flags, aji, S, N, s); break;
+            case 4: launch_v2<MODE, 4>(c, rb, re, flags, aji, S, N, s); break;
+            default: launch_v2<MODE, 5>(c, rb, re, flags, aji, S, N, s); break;
+        }
+        return;
+    }
+    if (c->rows_kernel == RK_PL) {
+        const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
+        const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+#ifdef PFAAI_DIAGNOSTICS
+        if (MODE == 0 && kw == 5 && !c->windows && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+            const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
+            const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
+            auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
+                               chunk, -1, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
+                               static_cast<unsigned long long*>(c->dbg.p));
+            return;
+        }
+#endif
+        // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
+        const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
+        if (nl) {
+            switch (kw) {
+                case 1: launch_pl<MODE, 1, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 2: launch_pl<MODE, 2, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 3: launch_pl<MODE, 3, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 4: launch_pl<MODE, 4, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                default: launch_pl<MODE, 5, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+            }
+            return;
+        }
+        switch (kw) {
+            case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 4: launch_pl<MODE, 4, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            default: launch_pl<MODE, 5, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+        }
+    } else if (c->rows_kernel == RK_PL512) {
+        switch (pick_kw<512>(c->max_cols, 10)) {
+            PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
+            PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
+            default: break;
+        }
+    } else {
+        switch (pick_kw<kRowThreads>(c->max_cols, 10)) {
+            KR_CASE(1) KR_CASE(2) KR_CASE(3) KR_CASE(4) KR_CASE(5) KR_CASE(6) KR_CASE(8) KR_CASE(10)
+            case 7: launch_k_rows<MODE, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 9: launch_k_rows<MODE, 10>(c, rb, re, flags, aji, S, N, s); break;
+            default: break;
+        }
+    }
+#undef PL_CASE
+#undef KR_CASE
+}
+
+}  // namespace pfaai_impl

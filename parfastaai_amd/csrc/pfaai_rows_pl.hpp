@@ -107,7 +107,14 @@ constexpr int kClkBlocks = 256;
 
 // NL: the per-column counts N live in LDS (u8 pairs, P <= 255) instead of
 // registers -- 5 VGPRs less at KW = 5, paid for with half the task capacity.
-template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false>
+// S5F: S5 (normalise protein i-1) runs FIRST in iteration i, on T words
+// loaded during iteration i-1.  At KW = 5 the 64-VGPR budget spills a few fp64
+// accumulators; their reloads in S5 are scratch loads, and gfx9 waits for
+// vector loads in order, so an S5 after the prefetches waited for the
+// members and run-table entries just issued (s_waitcnt vmcnt(0)) -- first, it
+// waits only for loads of the previous iteration, needed by now anyway.
+template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false,
+          bool S5F = false>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
                                                    uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
@@ -255,15 +262,48 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             tprev = t;
         }
     };
+    // S5 of protein i-1 on counter row (i-1)&1 with its T words (fp64,
+    // ascending protein order per pair)
+    auto s5 = [&](int i, const uint32_t (&tw)[KW], int32_t ta) {
+        if (!(i >= 1 && glen(i - 1) > 0u)) return;
+        uint32_t* acc_p = acc + ((i - 1) & 1) * W;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const int32_t w = tid + k * NT;
+            if (w < ncw) {
+                const uint32_t v = acc_p[w];
+                if (v) {
+                    acc_p[w] = 0u;
+                    const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+                    ev += (uint32_t)(c0 + c1);
+                    if constexpr (NL) n16[w] = (uint16_t)(n16[w] + (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 8));
+                    if (c0) {
+                        S[2 * k] += exact_div_any((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
+                        if constexpr (!NL) N[k] += 1u;
+                    }
+                    if (c1) {
+                        S[2 * k + 1] += exact_div_any((double)c1, (double)(ta + (int32_t)(tw[k] >> 16) - c1));
+                        if constexpr (!NL) N[k] += 1u << 16;
+                    }
+                }
+            }
+        }
+    };
+    uint32_t twc[KW];  // S5F: T words of the previous protein, carried across the barrier
+#pragma unroll
+    for (int k = 0; k < KW; ++k) twc[k] = 0u;
+    int32_t tac = 0;
+
 #pragma unroll 1
     for (int i = 0; i <= P; ++i) {
         const int st = i & 1, cs = i % 3;
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
-        const bool has_p = i >= 1 && glen(i - 1) > 0u;
-        // T(i-1): T16 words of the thread's columns and T[p][A], issued
-        // first so that S5 waits for nothing issued after them
-        const int pt = i >= 1 ? i - 1 : 0;
+        if constexpr (S5F) s5(i, twc, tac);
+        // T words of the thread's columns and T[p][A] (S5F: of protein i, for
+        // the next iteration; else of protein i-1, issued first so that S5
+        // waits for nothing issued after them)
+        const int pt = S5F ? min(i, P - 1) : (i >= 1 ? i - 1 : 0);
         if (prio & 1u) __builtin_amdgcn_s_setprio(2);  // loads issue ahead of other waves' S5 (flags bits 16-17)
         uint32_t tw[KW];
         const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
@@ -282,30 +322,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         s1(i + 3, gt);
         stamp(2);
         if (prio) __builtin_amdgcn_s_setprio(0);
-        // S5: normalise protein i-1 (fp64, ascending protein order per pair)
-        if (has_p) {
-            uint32_t* acc_p = acc + (st ^ 1) * W;
+        // S5: normalise protein i-1
+        if constexpr (!S5F) {
+            s5(i, tw, ta);
+        } else {
 #pragma unroll
-            for (int k = 0; k < KW; ++k) {
-                const int32_t w = tid + k * NT;
-                if (w < ncw) {
-                    const uint32_t v = acc_p[w];
-                    if (v) {
-                        acc_p[w] = 0u;
-                        const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                        ev += (uint32_t)(c0 + c1);
-                        if constexpr (NL) n16[w] = (uint16_t)(n16[w] + (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 8));
-                        if (c0) {
-                            S[2 * k] += exact_div_small((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
-                            if constexpr (!NL) N[k] += 1u;
-                        }
-                        if (c1) {
-                            S[2 * k + 1] += exact_div_small((double)c1, (double)(ta + (int32_t)(tw[k] >> 16) - c1));
-                            if constexpr (!NL) N[k] += 1u << 16;
-                        }
-                    }
-                }
-            }
+            for (int k = 0; k < KW; ++k) twc[k] = tw[k];
+            tac = ta;
         }
         stamp(3);
         if (prio & 2u) __builtin_amdgcn_s_setprio(1);

@@ -90,4 +90,14 @@ __device__ __forceinline__ double exact_div_small(double c, double dd) {
     return __builtin_fma(r, y, q);
 }
 
+// c / d for any denominator the row kernels meet: the fast path on its
+// verified domain (c <= d always holds for T[p][A] + T[p][B] - c with the
+// true T columns), IEEE '/' otherwise -- only the reference's QT T-index
+// quirk (PFAAI_FLAG_REF_COMPAT) pairs other genomes' counts
+// and can give d < c, d == 0 (inf, as the reference) or d < 0.
+__device__ __forceinline__ double exact_div_any(double c, double dd) {
+    if (__builtin_expect(dd < c, 0)) return c / dd;
+    return exact_div_small(c, dd);
+}
+
 }  // namespace pfaai

@@ -257,7 +257,7 @@ int dump_genomes(const std::string& prefix, const LoadedArrays& arr) {
     return ok ? 0 : 1;
 }
 
-const char* kRowsKernelName[] = {"k_rows_pl", "k_rows_pl512", "k_rows(fused)", "k_rows(worklist)"};
+const char* kRowsKernelName[] = {"k_rows_pl", "k_rows_pl512", "k_rows(fused)", "k_rows(worklist)", "k_rows_v2"};
 
 // The loader: G from `<p>_genomes` unless --loader tetras / --dump-arrays, or
 // a blob that is not a set (then the `<p>_tetras` F, as the reference reads).
@@ -303,7 +303,7 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         const int rk = impl.rowsKernel();
         std::printf("AJI (MI355X x%d)     : %10.2f ms  (load %.2f ms; |E| = %lld; %s: run tables %.2f ms, rows %.2f ms)\n",
                     impl.nDevices(), ms_since(t0), std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                    (long long)impl.nEvents(), rk >= 0 && rk < 4 ? kRowsKernelName[rk] : "?", impl.msBuild(),
+                    (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?", impl.msBuild(),
                     impl.msRows());
         if (app.pathToOutputFile.empty()) return 0;
         t1 = std::chrono::steady_clock::now();

@@ -37,15 +37,28 @@ def _newer(out, srcs):
 
 
 def build_hip(force=False, diag=False):
-    src = os.path.join(ROOT, "parfastaai_amd/csrc/pfaai_hip.hip")
+    """libpfaai_hip.so from the translation units of parfastaai_amd/csrc
+    (the C-ABI unit and one row-kernel unit per mode), compiled in parallel
+    to objects under build/ and linked."""
     csrc = os.path.join(ROOT, "parfastaai_amd/csrc")
+    units = sorted(f for f in os.listdir(csrc) if f.endswith(".hip"))
     deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include/pfaai_hip.h")]
     out = os.path.join(ROOT, "parfastaai_amd/lib", "libpfaai_hip_diag.so" if diag else "libpfaai_hip.so")
-    if force or _newer(out, deps):
-        os.makedirs(os.path.dirname(out), exist_ok=True)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-              "-ffp-contract=off", "-fno-fast-math", "-Wall", "-I" + os.path.join(ROOT, "include"),
-              *(["-DPFAAI_DIAGNOSTICS"] if diag else []), "-o", out, src])
+    if not (force or _newer(out, deps)):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    objdir = os.path.join(ROOT, "build", "hip_diag" if diag else "hip")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+             "-I" + os.path.join(ROOT, "include"), *(["-DPFAAI_DIAGNOSTICS"] if diag else [])]
+    objs = [os.path.join(objdir, u[:-4] + ".o") for u in units]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=min(len(units), int(os.environ.get("MAX_JOBS", "8")))) as ex:
+        futs = [ex.submit(_run, [HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)]) for u, o in zip(units, objs)]
+        for f in futs:
+            f.result()  # re-raises a failed compile
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
     return out
 
 

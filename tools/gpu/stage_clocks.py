@@ -1,6 +1,11 @@
-"""k_rows_pl stage clocks at 10k (PFAAI_PL_CLK=1, diagnostics library:
-`python tools/build_native.py --diag`, loaded through PFAAI_HIP_LIB): where the protein loop's
-time goes, per stage, for the waves of the first 256 workgroups."""
+"""Row-kernel stage clocks (diagnostics library: `python tools/build_native.py
+--diag`, loaded through PFAAI_HIP_LIB): where the protein loop's time goes,
+per stage, for the waves of the first 256 workgroups of the launch.
+
+    python tools/gpu/stage_clocks.py [--genomes 10000] [--v2] [--rows lo:hi]
+k_rows_pl (PFAAI_PL_CLK) by default, k_rows_v2 (PFAAI_V2_CLK) with --v2.
+"""
+import argparse
 import os
 
 os.environ.setdefault("PFAAI_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
@@ -14,24 +19,44 @@ import torch  # noqa: E402,F401
 from parfastaai_amd import _capi, syn  # noqa: E402
 from parfastaai_amd.datastruct import ParFAAIData  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-g = syn.generate(n, 100)
+ap = argparse.ArgumentParser()
+ap.add_argument("--genomes", type=int, default=10000)
+ap.add_argument("--v2", action="store_true")
+ap.add_argument("--rows", default=None, help="row range lo:hi (default: all rows)")
+a = ap.parse_args()
+g = syn.generate(a.genomes, 100)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
 eng = _capi.Engine(0)
 eng.load(**ds.problem())
 rows, pairs = eng.shape()
+r0, r1 = (int(x) for x in a.rows.split(":")) if a.rows else (0, rows)
 d = eng.alloc(pairs * 8)
-eng.run(0, rows, 0, d)  # warm
-eng.debug_clocks(arm=True)
-os.environ["PFAAI_PL_CLK"] = "1"
+if a.v2:
+    os.environ["PFAAI_ROWS_KERNEL"] = "v2"
+eng.run(r0, r1, 0, d)  # warm
 eng.timing(reset=True)
-eng.run(0, rows, 0, d)
+eng.run(r0, r1, 0, d)
+_, _, r_plain = eng.timing(reset=True)
+eng.debug_clocks(arm=True)
+os.environ["PFAAI_V2_CLK" if a.v2 else "PFAAI_PL_CLK"] = "1"
+eng.run(r0, r1, 0, d)
 _, b, r = eng.timing(reset=True)
 c = eng.debug_clocks().astype(np.float64)
-names = ["T + S4a issue", "S3 tasks", "S2/S1 issue", "S5 normalise", "S4b round 1", "S4b rounds 2+/whole", "recycle+barrier"]
+if a.v2:
+    names = ["T issue + S3", "M/S2/S1 issue", "S5 normalise", "S4 prefetched", "S4 further rounds", "long runs",
+             "barrier"]
+else:
+    names = ["T + S4a issue", "S3 tasks", "S2/S1 issue", "S5 normalise", "S4b round 1", "S4b rounds 2+/whole",
+             "recycle+barrier"]
+used = c[:, 0, :7].sum(axis=1) > 0
+c = c[used]
 tot = c[:, :, :7].sum(axis=2)
-print(f"row kernel {r:.3f} ms (clock variant); per wave-loop total: median {np.median(tot):.0f} cycles")
+print(f"{'k_rows_v2' if a.v2 else 'k_rows_pl'} rows [{r0}, {r1}): {r_plain:.3f} ms plain, {r:.3f} ms clock variant; "
+      f"{used.sum()} workgroups sampled; per wave-loop total: median {np.median(tot):.0f} cycles")
 for j, nm in enumerate(names):
     x = c[:, :, j]
-    print(f"  {nm:22s} share {x.sum() / tot.sum():6.3f}   wave0 {x[:, 0].mean():10.0f}   wave15 {x[:, 15].mean():10.0f}")
+    print(f"  {nm:22s} share {x.sum() / tot.sum():6.3f}   wave0 {x[:, 0].mean():10.0f}   wave15 {x[:, 15].mean():10.0f}"
+          f"   max-wave {x.max(axis=1).mean():10.0f}")
+if a.v2:
+    print(f"  further rounds per wave-row: mean {c[:, :, 7].mean():.1f}  max {c[:, :, 7].max():.0f}")
 eng.free(d)

@@ -1,0 +1,9 @@
+// ISA probe: the benchmark instantiation of k_rows_pl alone, so its VGPR /
+// spill / waitcnt shape can be read in seconds:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off --offload-device-only -S \
+//         -I include -o /tmp/probe.s tools/isa/probe_rows_pl.hip
+#include "../../parfastaai_amd/csrc/pfaai_rows_pl.hpp"
+
+template __global__ void pfaai::k_rows_pl<0, 5, 1024, 8, false, true, false, true>(
+    pfaai::Dev, int64_t, int32_t, int32_t, uint32_t, const unsigned long long*, double*, double*, int32_t*,
+    unsigned long long*, unsigned long long*);
