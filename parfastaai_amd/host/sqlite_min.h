@@ -15,6 +15,10 @@ int sqlite3_prepare_v2(sqlite3* db, const char* zSql, int nByte, sqlite3_stmt** 
 int sqlite3_step(sqlite3_stmt*);
 int sqlite3_finalize(sqlite3_stmt* pStmt);
 int sqlite3_bind_int(sqlite3_stmt*, int, int);
+int sqlite3_bind_double(sqlite3_stmt*, int, double);
+int sqlite3_bind_text(sqlite3_stmt*, int, const char*, int, void (*)(void*));
+int sqlite3_bind_blob(sqlite3_stmt*, int, const void*, int, void (*)(void*));
+int sqlite3_reset(sqlite3_stmt* pStmt);
 int sqlite3_column_int(sqlite3_stmt*, int iCol);
 const void* sqlite3_column_blob(sqlite3_stmt*, int iCol);
 int sqlite3_column_bytes(sqlite3_stmt*, int iCol);
@@ -29,3 +33,6 @@ constexpr int SQLITE_ROW = 100;
 constexpr int SQLITE_DONE = 101;
 constexpr int SQLITE_OPEN_READONLY = 0x00000001;
 constexpr int SQLITE_OPEN_URI = 0x00000040;
+constexpr int SQLITE_OPEN_READWRITE = 0x00000002;
+constexpr int SQLITE_OPEN_CREATE = 0x00000004;
+#define PFAAI_SQLITE_TRANSIENT (reinterpret_cast<void (*)(void*)>(-1))

@@ -131,3 +131,21 @@ def test_cli_both_loaders_same_bytes(tmp_path, loader):
     r = run(db, str(tmp_path / "b.csv"), "-r", q, "--loader", loader, "--ref-compat", "--bin", str(tmp_path / "b"))
     assert "k_rows_pl:" in r.stdout, r.stdout
     assert np.array_equal(fm.read_vec_f64(str(tmp_path / "b_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
+
+
+@pytest.mark.parametrize("compat", [[], ["--ref-compat"]], ids=["default", "ref-compat"])
+def test_cli_c1_rebuilt_db(tmp_path, compat):
+    """Config C1 end to end: the reference's 20-genome DB (rebuilt from its
+    fixtures, tests/test_c1_loader.py) through par_fastaai_amd -- CSV byte-
+    identical to the reference's xanthodb_aji_matrix_wheader.csv, and the -q
+    run to qsub_test_output_matrix_wheader.csv."""
+    from test_c1_loader import rebuild_xantho
+    db = rebuild_xantho(str(tmp_path))
+    out = tmp_path / "o.csv"
+    r = run(db, str(out), *compat)
+    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert out.read_text() == text("xanthodb_aji_matrix_wheader.csv")
+    q = tmp_path / "q.txt"
+    q.write_text(text("qsub_test_input.txt"))
+    run(db, str(out), "-q", str(q), *compat)
+    assert out.read_text() == text("qsub_test_output_matrix_wheader.csv")

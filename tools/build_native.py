@@ -6,6 +6,7 @@
                                                 built only on request: --diag)
   cli      parfastaai_amd/lib/par_fastaai_amd   g++ host CLI over the C ABI
   syn      tools/_build/libpfaai_syn.so         synthetic DB generator
+  rebuild  tools/_build/rebuild_xantho_db       C1 DB from the reference's fixtures
   oracle   oracle/_build/libpfaai_oracle.so     CPU oracle (test infra)
   ref      oracle/_ref/par_fastaai.x            the reference, from its own
                                                 sources (only where
@@ -71,6 +72,15 @@ def build_syn(force=False):
     return out
 
 
+def build_rebuild_tool(force=False):
+    src = os.path.join(ROOT, "tools/rebuild_xantho_db.cpp")
+    out = os.path.join(ROOT, "tools/_build/rebuild_xantho_db")
+    if force or _newer(out, [src, os.path.join(ROOT, "parfastaai_amd/host/sqlite_min.h")]):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-o", out, src, "/lib/x86_64-linux-gnu/libsqlite3.so.0"])
+    return out
+
+
 def build_oracle(force=False):
     src = os.path.join(ROOT, "oracle/pfaai_oracle.c")
     out = os.path.join(ROOT, "oracle/_build/libpfaai_oracle.so")
@@ -104,7 +114,7 @@ def build_ref(force=False):
 
 
 def build_all(force=False):
-    outs = [build_hip(force), build_syn(force), build_oracle(force), build_cli(force)]
+    outs = [build_hip(force), build_syn(force), build_oracle(force), build_cli(force), build_rebuild_tool(force)]
     try:
         outs.append(build_ref(force))
     except subprocess.CalledProcessError as e:  # the reference build is optional
