@@ -719,6 +719,8 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
     }
     int rc = ensure(c, c->scalars, SC_N * sizeof(unsigned long long));
     if (rc) {
+        release(c->scalars);
+        (void)hipStreamDestroy(c->stream);
         delete c;
         return rc;
     }

@@ -18,18 +18,11 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
-    // S5 first in the protein loop (k_rows_pl S5F); PFAAI_PL_S5F=0 for the old order (A/B)
-    const char* s5e = getenv("PFAAI_PL_S5F");
-    const bool s5f = !(s5e && s5e[0] == '0');
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
-#define PLK(BF, SF)                                                                                                  \
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, BF, SF>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, \
-                       chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
-        if (bigf) {
-            if (s5f) PLK(true, true); else PLK(true, false);
-        } else {
-            if (s5f) PLK(false, true); else PLK(false, false);
-        }
+#define PLK(BF)                                                                                                      \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, BF>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, \
+                       abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+        if (bigf) PLK(true); else PLK(false);
 #undef PLK
     };
     if (nchunks == 1 || !c->windows) {

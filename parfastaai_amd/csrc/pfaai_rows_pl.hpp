@@ -114,7 +114,7 @@ constexpr int kClkBlocks = 256;
 // members and run-table entries just issued (s_waitcnt vmcnt(0)) -- first, it
 // waits only for loads of the previous iteration, needed by now anyway.
 template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false,
-          bool S5F = false>
+          bool S5F = true>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
                                                    uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
@@ -277,12 +277,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     ev += (uint32_t)(c0 + c1);
                     if constexpr (NL) n16[w] = (uint16_t)(n16[w] + (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 8));
+                    const int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
                     if (c0) {
-                        S[2 * k] += exact_div_any((double)c0, (double)(ta + (int32_t)(tw[k] & 0xFFFFu) - c0));
+                        S[2 * k] += exact_div_any((double)c0, (double)d0);
                         if constexpr (!NL) N[k] += 1u;
                     }
                     if (c1) {
-                        S[2 * k + 1] += exact_div_any((double)c1, (double)(ta + (int32_t)(tw[k] >> 16) - c1));
+                        S[2 * k + 1] += exact_div_any((double)c1, (double)d1);
                         if constexpr (!NL) N[k] += 1u << 16;
                     }
                 }
