@@ -199,6 +199,10 @@ int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
                        double* h_aji, double* h_S, int32_t* h_N);
 
+/* Wall times (ms) of the last pfaai_load: host-side checks, H2D copies, and
+ * the device-side F / G build (or G-covers-F check) up to its completion. */
+int pfaai_load_timing(const pfaai_ctx* ctx, double* ms_checks, double* ms_upload, double* ms_device);
+
 /* Which row kernel the last pfaai_run launched (PFAAI_ROWS_*) and whether it
  * ran by absolute column windows (rows wider than one kernel chunk). */
 int pfaai_run_info(const pfaai_ctx* ctx, int32_t* rows_kernel, int32_t* column_windows);

@@ -33,7 +33,7 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info",
+    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_load_timing",
 ]
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
 
@@ -97,6 +97,8 @@ def load_library():
         "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
         "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "pfaai_load_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     }
@@ -240,6 +242,13 @@ class Engine:
         self._check(self.lib.pfaai_run_info(self.ctx, ctypes.byref(rk), ctypes.byref(win)), "pfaai_run_info")
         return {"n_events": ne.value, "ms_build": mb.value, "ms_rows": mr.value,
                 "rows_kernel": ROWS_KERNELS.get(rk.value, "?"), "column_windows": bool(win.value)}
+
+    def load_timing(self):
+        """(ms host checks, ms H2D, ms device F/G build) of the last load."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        self._check(self.lib.pfaai_load_timing(self.ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                    "pfaai_load_timing")
+        return a.value, b.value, c.value
 
     def timing(self, reset=True):
         """(n_runs, ms_build_total, ms_rows_total) of the runs since the last reset."""

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +46,7 @@ struct pfaai_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     bool loaded = false;
+    double load_ms[3] = {0, 0, 0};  // last pfaai_load: host checks, H2D uploads, device F/G build (+ sync)
 
     // problem (host copies of scalars + small maps)
     pfaai_problem prob{};

@@ -397,6 +397,10 @@ void release_sort_space(pfaai_ctx* c) {
 int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     HIPCHK(c, hipSetDevice(c->device));
     c->loaded = false;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    double ms_upload = 0.0;
     const pfaai_problem& p = *pb;
     if (p.mode < 0 || p.mode > 2) return fail(c, PFAAI_RC_INVALID, "mode must be 0, 1 or 2");
     if (p.n_ids < 2 || p.n_prot < 1 || p.n_prot >= kMaxRuns || p.t_cols < 1)
@@ -574,6 +578,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
 
     int rc;
     hipStream_t s = c->stream;
+    const auto t1 = clk::now();  // host checks done
     if ((rc = upload(c, c->T, p.T, tn))) return rc;
     std::vector<uint8_t> isq(ni, 1);
     if (p.is_q) isq.assign(p.is_q, p.is_q + ni);
@@ -619,9 +624,10 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         if ((rc = upload(c, c->Lp, p.Lp, PFAAI_NTETRAMERS + 1))) return rc;
         if ((rc = upload(c, c->Fp, p.F_prot, n_f))) return rc;
         if ((rc = upload(c, c->Fg, p.F_genome, n_f))) return rc;
-    } else if ((rc = build_f_from_g(c, ng, n_f, s))) {
-        return rc;
     }
+    const auto t2 = clk::now();  // uploads done (hipMemcpy is synchronous)
+    ms_upload = ms(t1, t2);
+    if (!in_f && (rc = build_f_from_g(c, ng, n_f, s))) return rc;
     bool has_g = in_g;
     if (in_g && in_f && n_f) {  // both given: G must hold F's memberships (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
@@ -692,6 +698,10 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[c->row_genome_h[r]];
     HIPCHK(c, hipMemsetAsync(c->scalars.p, 0, SC_N * sizeof(unsigned long long), s));
     HIPCHK(c, hipStreamSynchronize(s));
+    const auto t3 = clk::now();
+    c->load_ms[0] = ms(t0, t1);
+    c->load_ms[1] = ms_upload;
+    c->load_ms[2] = ms(t2, t3);
     release_sort_space(c);  // pfaai_run never allocates; the work-list path re-allocates below
     if (!has_g && (rc = ensure_worklists(c))) return rc;
     c->loaded = true;
@@ -863,6 +873,14 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     if (h_S) HIPCHK(c, hipMemcpyAsync(h_S, S, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (h_N) HIPCHK(c, hipMemcpyAsync(h_N, N, np * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_RC_OK;
+}
+
+int pfaai_load_timing(const pfaai_ctx* c, double* ms_checks, double* ms_upload, double* ms_device) {
+    if (!c || !c->loaded) return PFAAI_RC_INVALID;
+    if (ms_checks) *ms_checks = c->load_ms[0];
+    if (ms_upload) *ms_upload = c->load_ms[1];
+    if (ms_device) *ms_device = c->load_ms[2];
     return PFAAI_RC_OK;
 }
 

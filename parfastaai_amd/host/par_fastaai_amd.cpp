@@ -300,11 +300,17 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         }
         auto t1 = std::chrono::steady_clock::now();
         impl.run();
+        const double ms_run = ms_since(t1);
         const int rk = impl.rowsKernel();
-        std::printf("AJI (MI355X x%d)     : %10.2f ms  (load %.2f ms; |E| = %lld; %s: run tables %.2f ms, rows %.2f ms)\n",
-                    impl.nDevices(), ms_since(t0), std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                    (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?", impl.msBuild(),
-                    impl.msRows());
+        std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; %s)\n", impl.nDevices(), ms_since(t0),
+                    (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?");
+        double lc = 0, lu = 0, ld = 0;
+        pfaai_load_timing(impl.context(), &lc, &lu, &ld);
+        const double ms_ctor = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        std::printf("  breakdown         : context %.1f + load checks %.1f, H2D %.1f, device F/G %.1f ms; run %.1f ms = "
+                    "run tables %.2f + %s %.2f + D2H / JAC fill %.1f ms\n",
+                    ms_ctor - lc - lu - ld, lc, lu, ld, ms_run, impl.msBuild(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?",
+                    impl.msRows(), ms_run - impl.msBuild() - impl.msRows());
         if (app.pathToOutputFile.empty()) return 0;
         t1 = std::chrono::steady_clock::now();
         std::printf("Writing output with %lld query genomes and %lld target genomes. \n",

@@ -38,7 +38,7 @@ def test_cli_csv_bytes(tmp_path, name, devs):
     out = tmp_path / "out.csv"
     r = run(db, str(out), "--bin", str(tmp_path / "o"), *devs)
     # the drop-in runs the benchmarked path: <p>_genomes -> G, F built on the GPU, k_rows_pl
-    assert "<p>_genomes -> G" in r.stdout and "k_rows_pl:" in r.stdout, r.stdout
+    assert "<p>_genomes -> G" in r.stdout and "; k_rows_pl)" in r.stdout, r.stdout
     assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
     J = fm.read_jac(str(tmp_path / "o_jac.bin"))
     Jr = fm.read_jac(gpath(name + "_jac.bin"))
@@ -126,10 +126,10 @@ def test_cli_both_loaders_same_bytes(tmp_path, loader):
     db = unpack(tmp_path, "xdb_subset1.db")
     q = unpack(tmp_path, "xdb_subset2.db")
     r = run(db, str(tmp_path / "a.csv"), "--loader", loader)
-    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert "; k_rows_pl)" in r.stdout, r.stdout
     assert (tmp_path / "a.csv").read_text() == text("xdb_subset1_aji_matrix_wheader.csv")
     r = run(db, str(tmp_path / "b.csv"), "-r", q, "--loader", loader, "--ref-compat", "--bin", str(tmp_path / "b"))
-    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert "; k_rows_pl)" in r.stdout, r.stdout
     assert np.array_equal(fm.read_vec_f64(str(tmp_path / "b_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
 
 
@@ -143,7 +143,7 @@ def test_cli_c1_rebuilt_db(tmp_path, compat):
     db = rebuild_xantho(str(tmp_path))
     out = tmp_path / "o.csv"
     r = run(db, str(out), *compat)
-    assert "k_rows_pl:" in r.stdout, r.stdout
+    assert "; k_rows_pl)" in r.stdout, r.stdout
     assert out.read_text() == text("xanthodb_aji_matrix_wheader.csv")
     q = tmp_path / "q.txt"
     q.write_text(text("qsub_test_input.txt"))

@@ -52,7 +52,7 @@ def main():
         if p.returncode:
             print(out[-3000:], err[-3000:], file=sys.stderr)
             raise SystemExit(f"{cmd[0]} exited {p.returncode}")
-        return w, [l for l in out.splitlines() if ":" in l and ("ms" in l or "time" in l.lower())]
+        return w, [l.strip() for l in out.splitlines() if ":" in l and ("ms" in l or "time" in l.lower())]
 
     ours_csv, ref_csv = os.path.join(a.workdir, "ours.csv"), os.path.join(a.workdir, "ref.csv")
     w_ours, l_ours = run([os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd"), db, ours_csv])
