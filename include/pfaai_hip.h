@@ -61,6 +61,11 @@ enum { PFAAI_MODE_ALL = 0, PFAAI_MODE_QSUB = 1, PFAAI_MODE_QT = 2 };
 #define PFAAI_FLAG_KEEP_RUNS 4u  /* reuse the run table an earlier pfaai_run on this
                                     load built (same stream or ordered after it):
                                     row tiles / pipelined shards pay k_blk once */
+#define PFAAI_FLAG_FULL_ROWS 8u  /* pfaai_run writes the rows of printOutput's dense
+                                    matrix (main.cpp:143-154) instead of JAC pairs:
+                                    out[row * n_cols + col], n_cols = n_ids (ALL,
+                                    QSUB: every genome) or n_tgt (QT), the mirror
+                                    half included, the diagonal left unwritten */
 
 /* Row kernels (pfaai_run_info): k_rows_pl (genome-major walk), its 512-
  * thread form, the fused k_rows (G lists > 1024 entries), the work-list
@@ -186,7 +191,26 @@ typedef int (*pfaai_sink_fn)(void* user, int64_t row_begin, int64_t row_end, int
                              int64_t count, const double* aji, const double* S, const int32_t* N);
 int pfaai_stream(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, int64_t tile_pairs,
                  uint32_t flags, pfaai_sink_fn sink, void* user);
-/* |E| summed over the tiles of the last pfaai_stream. */
+/*
+ * Dense output rows (the streamed CSV of config C5): rows [row_begin,
+ * row_end) of printOutput's nQ x nT AJI matrix (main.cpp:133-175) -- ALL:
+ * N x N with the mirror half and a zero diagonal; QSUB: query rows in
+ * query-file order x all genomes, query-query cells mirrored; QT: queries x
+ * targets -- in tiles of at most tile_rows rows.  Every row is computed whole
+ * (AJI(A, B) and AJI(B, A) are bit-identical: the same counts, denominators
+ * and protein order), so no tile depends on another; tile k computes while
+ * tile k-1 is copied to pinned host memory, and
+ *   sink(user, tile_row_begin, tile_row_end, n_cols, block)
+ * gets block[(r - tile_row_begin) * n_cols + col] in row order on the calling
+ * thread (valid during the call).  A non-zero sink return stops the stream
+ * and is returned.  |E| of the tiles (pfaai_stream_events) counts every
+ * (p, A, B) of the full rows, i.e. both orientations of a pair.
+ */
+typedef int (*pfaai_matrix_sink_fn)(void* user, int64_t row_begin, int64_t row_end, int64_t n_cols,
+                                    const double* block);
+int pfaai_stream_matrix(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, int64_t tile_rows, uint32_t flags,
+                        pfaai_matrix_sink_fn sink, void* user);
+/* |E| summed over the tiles of the last pfaai_stream / pfaai_stream_matrix. */
 int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 
 /* ParFAAIImpl::run() (algorithm_impl.hpp:325-329) for a block of rows:

@@ -210,6 +210,18 @@ class ParFAAIHipImpl {
         pfaai_stream_events(ctx(), &m_events);
         return ok ? 0 : PFAAI_RC_INVALID;
     }
+    // Dense output rows (pfaai_stream_matrix): printOutput's nQ x nT matrix
+    // (main.cpp:143-154), mirror half included, tile by tile to
+    // sink(user, row_begin, row_end, n_cols, block) -- the whole matrix is
+    // never held.  Returns 0 or throws the engine error.
+    int streamMatrix(int64_t tile_rows, pfaai_matrix_sink_fn sink, void* user) {
+        int64_t rows = 0;
+        int rc = pfaai_shape(ctx(), &rows, nullptr);
+        if (!rc) rc = pfaai_stream_matrix(ctx(), 0, rows, tile_rows, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, sink, user);
+        if (rc) throw HipError(rc, pfaai_last_error(ctx()));
+        pfaai_stream_events(ctx(), &m_events);
+        return 0;
+    }
     const std::vector<JACType>& getJAC() const { return m_JAC; }
     const std::vector<ValueType>& getAJI() const { return m_AJI; }
     // the reference's debug listing (algorithm_impl.hpp:347-356; main.cpp

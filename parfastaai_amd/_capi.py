@@ -26,6 +26,7 @@ MODE_ALL, MODE_QSUB, MODE_QT = 0, 1, 2
 FLAG_REF_COMPAT = 1
 FLAG_EMIT_JAC = 2
 FLAG_KEEP_RUNS = 4
+FLAG_FULL_ROWS = 8
 
 # every symbol include/pfaai_hip.h declares
 EXPORTS = [
@@ -33,7 +34,7 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_load_timing",
+    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_load_timing", "pfaai_stream_matrix",
 ]
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
 
@@ -42,6 +43,10 @@ ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
 SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                            ctypes.c_int64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                            ctypes.POINTER(ctypes.c_int32))
+
+# int sink(void* user, i64 row_begin, i64 row_end, i64 n_cols, const double* block)  (pfaai_matrix_sink_fn)
+MATRIX_SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.POINTER(ctypes.c_double))
 
 
 class PfaaiError(RuntimeError):
@@ -96,6 +101,7 @@ def load_library():
         "pfaai_build_f": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, vp, vp, vp, vp, vp]),
         "pfaai_stream": (ctypes.c_int, [vp, i64, i64, i64, u32, SINK_FN, vp]),
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
+        "pfaai_stream_matrix": (ctypes.c_int, [vp, i64, i64, i64, u32, MATRIX_SINK_FN, vp]),
         "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pfaai_load_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
@@ -230,6 +236,30 @@ class Engine:
         if err:
             raise err[0]
         self._check(rc, "pfaai_stream")
+        ne = ctypes.c_int64()
+        self._check(self.lib.pfaai_stream_events(self.ctx, ctypes.byref(ne)), "pfaai_stream_events")
+        return ne.value
+
+    def stream_matrix(self, row_begin, row_end, tile_rows, flags, sink):
+        """Dense output rows (pfaai_stream_matrix): sink(row_begin, row_end,
+        block) gets a numpy view [rows, n_cols] of each tile in row order
+        (valid during the call); a truthy return stops the stream.  Returns
+        |E| over the tiles (both orientations of every pair)."""
+        err = []
+
+        def _cb(_user, rb, re, n_cols, block):
+            try:
+                a = np.ctypeslib.as_array(block, shape=(re - rb, n_cols))
+                return 7 if sink(rb, re, a) else 0
+            except Exception as e:  # surfaced after the call
+                err.append(e)
+                return 7
+
+        cb = MATRIX_SINK_FN(_cb)
+        rc = self.lib.pfaai_stream_matrix(self.ctx, row_begin, row_end, int(tile_rows), flags, cb, None)
+        if err:
+            raise err[0]
+        self._check(rc, "pfaai_stream_matrix")
         ne = ctypes.c_int64()
         self._check(self.lib.pfaai_stream_events(self.ctx, ctypes.byref(ne)), "pfaai_stream_events")
         return ne.value

@@ -53,7 +53,8 @@ struct pfaai_ctx {
     int64_t n_rows = 0, n_pairs = 0;
     std::vector<int32_t> row_genome_h;
     std::vector<int32_t> q_index_h;
-    int32_t max_cols = 0;
+    int32_t max_cols = 0;  // widest output row of the loaded mode
+    int32_t cols_run = 0;  // widest row of the current run (max_cols; n_ids for full rows)
 
     // device-resident problem
     DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
@@ -181,10 +182,10 @@ inline int pick_kw(int32_t max_cols, int kw_max) {
 
 // k_rows_pl's chunk width for this problem (launch_rows' KW choice)
 inline int64_t pl_chunk_cols(pfaai_ctx* c) {
-    if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->max_cols, 10);
-    if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->max_cols, 5);
+    if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->cols_run, 10);
+    if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->cols_run, 5);
     const char* km = getenv("PFAAI_PL_KWMAX");
-    return 2 * 1024 * (int64_t)pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+    return 2 * 1024 * (int64_t)pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 }
 
 // Row kernels for output rows [rb, re) (pfaai_launch.hpp; instantiated per

@@ -148,12 +148,31 @@ int build_records(pfaai_ctx* c, int64_t rb, int64_t re, hipStream_t s, bool firs
     return PFAAI_RC_OK;
 }
 
+// The lexicographically first E triple of the LOADED mode (the ref-compat
+// zero-overlap quirk) -- also for full-row runs, whose
+// mirror cells are the loaded mode's pairs.
+int launch_first_key(pfaai_ctx* c, hipStream_t s) {
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
+#define FK(M)                                                                                                       \
+    hipLaunchKernelGGL((k_entries<M, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev, (int64_t)0,       \
+                       (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),                  \
+                       static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err)
+    switch (c->prob.mode) {
+        case 0: FK(0); break;
+        case 1: FK(1); break;
+        default: FK(2); break;
+    }
+#undef FK
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_RC_OK;
+}
+
 // Fused genome-major path: only the run table (+ the first E triple for the
 // ref-compat zero-overlap quirk); k_rows walks the G lists itself.
 template <int MODE>
 int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    int* err = reinterpret_cast<int*>(sc + SC_ERR);
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
     const int dbg = DIAG_ENV("PFAAI_BLK_ABLATE") ? atoi(DIAG_ENV("PFAAI_BLK_ABLATE")) : 0;
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
@@ -167,10 +186,8 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
         hipLaunchKernelGGL((k_blk<false, 1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile,
                            dbg, 0, 1);
     if (first_event) {
-        HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
-        hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
-                           (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr), static_cast<uint2*>(nullptr),
-                           static_cast<const unsigned long long*>(nullptr), sc + SC_FIRST_KEY, err);
+        const int rc = launch_first_key(c, s);
+        if (rc) return rc;
     }
     HIPCHK(c, hipGetLastError());
     return PFAAI_RC_OK;
@@ -264,12 +281,8 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
                 hipLaunchKernelGGL((k_blk<true, 1024>), dim3(ceil_div(kNTetramers, win_tile)), dim3(1024), lds, s, dw,
                                    win_tile, 0, (int32_t)wcols, nwin);
             if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
-                int* err = reinterpret_cast<int*>(sc + SC_ERR);
-                HIPCHK(c, hipMemsetAsync(sc + SC_FIRST_KEY, 0xFF, sizeof(unsigned long long), s));
-                hipLaunchKernelGGL((k_entries<MODE, true>), dim3(kNTetramers), dim3(kTetraThreads), 0, s, c->dev,
-                                   (int64_t)0, (int64_t)0, static_cast<uint32_t*>(nullptr),
-                                   static_cast<uint2*>(nullptr), static_cast<const unsigned long long*>(nullptr),
-                                   sc + SC_FIRST_KEY, err);
+                const int rcf = launch_first_key(c, s);
+                if (rcf) return rcf;
             }
             HIPCHK(c, hipGetLastError());
             c->win_valid = true;
@@ -294,8 +307,12 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     // after the run that built it)
     const bool keep = !wl && (flags & PFAAI_FLAG_KEEP_RUNS) && c->runs_valid && (c->runs_key || !compat);
     int rc = PFAAI_RC_OK;
-    if (wl) rc = build_records<MODE>(c, rb, re, s, compat);
-    else if (!keep) {
+    if constexpr (MODE == kModeFull) {
+        if (wl) return fail(c, PFAAI_RC_INVALID, "full rows need the genome-major path");
+    } else if (wl) {
+        rc = build_records<MODE>(c, rb, re, s, compat);
+    }
+    if (!wl && !keep) {
         rc = build_runs_g<MODE>(c, s, compat);
         c->runs_valid = rc == PFAAI_RC_OK;
         c->runs_key = compat;
@@ -561,6 +578,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         c->n_pairs = (int64_t)p.n_qry * p.n_tgt;
         c->max_cols = p.n_tgt;
     }
+    c->cols_run = c->max_cols;
     for (int32_t g = 0; g < ni; ++g) { tcol_row[g] = g; tcol_col[g] = g; }
     // QT reference T-index quirk: the reference reads
     // T[p][i / nT] and T[p][nQ + i % nT] for JAC index i = q*nT + t.  Both
@@ -844,7 +862,12 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         c->pool_used = 0;
     }
     c->timed = true;
+    // full rows (pfaai_stream_matrix): every column of the loaded mode's
+    // target set; QT rows already are full rows
+    const bool full = (flags & PFAAI_FLAG_FULL_ROWS) && c->prob.mode != PFAAI_MODE_QT;
+    c->cols_run = full ? c->prob.n_ids : c->max_cols;
     if (rb == re) return PFAAI_RC_OK;
+    if (full) return run_mode<kModeFull>(c, rb, re, flags, aji, S, N, s);
     switch (c->prob.mode) {
         case 0: return run_mode<0>(c, rb, re, flags, aji, S, N, s);
         case 1: return run_mode<1>(c, rb, re, flags, aji, S, N, s);
@@ -1165,6 +1188,104 @@ static int stream_impl(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs,
     for (int64_t k = std::max<int64_t>(0, ntiles - 2); k < ntiles; ++k)
         if ((rc = deliver(k))) { drain(); return rc; }
     return PFAAI_RC_OK;
+}
+
+// Dense output rows (pfaai_stream_matrix): row tiles of printOutput's
+// matrix, each computed whole with PFAAI_FLAG_FULL_ROWS (no tile depends on
+// another), double-buffered like stream_impl: tile k computes into device
+// buffer k & 1 while tile k - 1 is copied to pinned buffer (k - 1) & 1 and
+// tile k - 2 is handed to the sink.  The run table is built by tile 0 only.
+static int stream_matrix_impl(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_rows, uint32_t flags,
+                              pfaai_matrix_sink_fn sink, void* user) {
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (!sink) return fail(c, PFAAI_RC_INVALID, "sink is required");
+    if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
+    if (flags & PFAAI_FLAG_EMIT_JAC) return fail(c, PFAAI_RC_INVALID, "pfaai_stream_matrix writes AJI only");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->st_events = 0;
+    if (rb == re) return PFAAI_RC_OK;
+    const bool qt = c->prob.mode == PFAAI_MODE_QT;
+    const int64_t n_cols = qt ? c->prob.n_tgt : c->prob.n_ids;
+    // QT under REF_COMPAT: the reference prints pair (q, t) at column
+    // mapTargetId(nQ + t) (its JAC ids, ds_impl.hpp:434-436 + main.cpp:149), i.e.
+    // each row rotated right by nQ; with nQ > nT its rows collide instead.
+    const bool rot = qt && (flags & PFAAI_FLAG_REF_COMPAT);
+    if (rot && c->prob.n_qry > c->prob.n_tgt)
+        return fail(c, PFAAI_RC_INVALID,
+                    "pfaai_stream_matrix: the reference's QT ids overlap rows when nQ > nT; use the default ids");
+    const int64_t shift = rot ? c->prob.n_qry % n_cols : 0;
+    tile_rows = std::max<int64_t>(1, std::min<int64_t>(tile_rows, re - rb));
+    const int64_t ntiles = ceil_div(re - rb, tile_rows);
+    const size_t per = (size_t)tile_rows * n_cols * sizeof(double);
+    int rc;
+    if ((rc = ensure(c, c->st_dev, 2 * per))) return rc;
+    const size_t host_bytes = 2 * per + (size_t)ntiles * sizeof(unsigned long long);
+    if (c->st_host_bytes < host_bytes) {
+        if (c->st_host) (void)hipHostFree(c->st_host);
+        c->st_host = nullptr;
+        c->st_host_bytes = 0;
+        HIPCHK(c, hipHostMalloc(&c->st_host, host_bytes, hipHostMallocDefault));
+        c->st_host_bytes = host_bytes;
+    }
+    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        if (!c->st_done[i]) HIPCHK(c, hipEventCreateWithFlags(&c->st_done[i], hipEventDisableTiming));
+        if (!c->st_copied[i]) HIPCHK(c, hipEventCreateWithFlags(&c->st_copied[i], hipEventDisableTiming));
+    }
+    auto dptr = [&](int b) { return reinterpret_cast<double*>(static_cast<char*>(c->st_dev.p) + b * per); };
+    auto hptr = [&](int b) { return reinterpret_cast<double*>(static_cast<char*>(c->st_host) + b * per); };
+    auto* evs = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->st_host) + 2 * per);
+    const auto* sc_ev = static_cast<unsigned long long*>(c->scalars.p) + SC_EVENTS;
+    auto tile = [&](int64_t k, int64_t& r0, int64_t& r1) {
+        r0 = rb + k * tile_rows;
+        r1 = std::min(re, r0 + tile_rows);
+    };
+    auto drain = [&]() {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->copy_stream);
+    };
+    auto deliver = [&](int64_t k) -> int {
+        const int b = (int)(k & 1);
+        HIPCHK(c, hipEventSynchronize(c->st_copied[b]));
+        int64_t r0, r1;
+        tile(k, r0, r1);
+        c->st_events += (int64_t)evs[k];
+        if (shift) {
+            double* h = hptr(b);
+            par_for(r1 - r0, [&](int64_t lo, int64_t hi, int) {
+                for (int64_t r = lo; r < hi; ++r)
+                    std::rotate(h + r * n_cols, h + r * n_cols + (n_cols - shift), h + (r + 1) * n_cols);
+            }, (r1 - r0) * n_cols);
+        }
+        const int src = sink(user, r0, r1, n_cols, hptr(b));
+        return src ? fail(c, src, "pfaai_stream_matrix: the sink stopped the stream") : PFAAI_RC_OK;
+    };
+    for (int64_t k = 0; k < ntiles; ++k) {
+        const int b = (int)(k & 1);
+        int64_t r0, r1;
+        tile(k, r0, r1);
+        const size_t bytes = (size_t)(r1 - r0) * n_cols * sizeof(double);
+        if (k >= 2 && (rc = deliver(k - 2))) { drain(); return rc; }
+        if (k >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, c->st_copied[b], 0));
+        if (!qt) HIPCHK(c, hipMemsetAsync(dptr(b), 0, bytes, c->stream));  // the diagonal stays 0 (main.cpp:143)
+        rc = pfaai_run(c, r0, r1, flags | PFAAI_FLAG_FULL_ROWS | (k ? PFAAI_FLAG_KEEP_RUNS : 0u), dptr(b) - r0 * n_cols,
+                       nullptr, nullptr, c->stream);
+        if (rc) { drain(); return rc; }
+        HIPCHK(c, hipMemcpyAsync(&evs[k], sc_ev, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->st_done[b], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->st_done[b], 0));
+        HIPCHK(c, hipMemcpyAsync(hptr(b), dptr(b), bytes, hipMemcpyDeviceToHost, c->copy_stream));
+        HIPCHK(c, hipEventRecord(c->st_copied[b], c->copy_stream));
+    }
+    for (int64_t k = std::max<int64_t>(0, ntiles - 2); k < ntiles; ++k)
+        if ((rc = deliver(k))) { drain(); return rc; }
+    return PFAAI_RC_OK;
+}
+
+int pfaai_stream_matrix(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_rows, uint32_t flags,
+                        pfaai_matrix_sink_fn sink, void* user) {
+    if (!c) return PFAAI_RC_INVALID;
+    return guarded(c, [&] { return stream_matrix_impl(c, rb, re, tile_rows, flags, sink, user); });
 }
 
 int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,

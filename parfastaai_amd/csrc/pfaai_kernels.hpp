@@ -88,10 +88,19 @@ __device__ __forceinline__ int64_t xcd_row(int64_t b, int64_t n, int64_t ch = kX
 // ---------------------------------------------------------------------------
 // mode index maps (ds_impl.hpp:83-96, 251-276, 411-426)
 // ---------------------------------------------------------------------------
+// MODE 3 (kModeFull) is not a reference mode: the full output row of
+// printOutput's dense matrix (main.cpp:143-154) for an all-vs-all or query-
+// subset row genome A -- every column B != A, the mirror half included,
+// written at row(A) * n_ids + B (pfaai_stream_matrix).  AJI(A, B) and
+// AJI(B, A) are bit-identical (the same counts, denominators and protein
+// order), so the mirror half equals the reference's mirrored copy.
+constexpr int kModeFull = 3;
+
 template <int MODE>
 __device__ __forceinline__ bool col_valid(const Dev& d, int32_t a, int32_t b) {
     if constexpr (MODE == 0) return b > a;
     else if constexpr (MODE == 1) return b != a && (!d.is_q[b] || b > a);
+    else if constexpr (MODE == kModeFull) return b != a;
     else return b < d.n_tgt;
 }
 
@@ -99,6 +108,8 @@ template <int MODE>
 __device__ __forceinline__ int64_t pair_index(const Dev& d, int32_t a, int32_t b, bool compat) {
     if constexpr (MODE == 0) {
         return (int64_t)d.n_ids * a + b - (int64_t)(a + 2) * (a + 1) / 2;
+    } else if constexpr (MODE == kModeFull) {
+        return (int64_t)d.row_of[a] * d.n_ids + b;
     } else if constexpr (MODE == 1) {
         if (!d.is_q[b]) return (int64_t)d.q_index[a] * d.n_tgt + d.t_rank[b];
         int64_t gia = d.q_index[a], gib = d.q_index[b];
@@ -114,7 +125,7 @@ __device__ __forceinline__ int64_t pair_index(const Dev& d, int32_t a, int32_t b
 template <int MODE>
 __device__ __forceinline__ void row_cols(const Dev& d, int32_t a, int32_t& lo, int32_t& hi) {
     if constexpr (MODE == 0) { lo = a + 1; hi = d.n_ids; }
-    else if constexpr (MODE == 1) { lo = 0; hi = d.n_ids; }
+    else if constexpr (MODE == 1 || MODE == kModeFull) { lo = 0; hi = d.n_ids; }
     else { lo = 0; hi = d.n_tgt; }
 }
 
@@ -552,6 +563,7 @@ __device__ __forceinline__ void scatter_one(const Dev& d, int32_t a, int32_t b, 
                                             int32_t cc1, uint32_t& ev) {
     if (b < 0) return;
     if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
+    if (MODE == kModeFull && b == a) return;
     if (b >= cc0 && b < cc1) {
         const uint32_t o = (uint32_t)(b - cc0);
         atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));

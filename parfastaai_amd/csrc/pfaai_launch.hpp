@@ -13,7 +13,7 @@ template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
-    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
     const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
@@ -50,7 +50,7 @@ template <int MODE, int KW>
 void launch_v2(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * kV2Threads;
-    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
     const size_t lds = (4 * (size_t)KW * kV2Threads + c->prob.n_prot + 1) * sizeof(uint32_t);  // u32 counters x 2
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
@@ -90,15 +90,15 @@ template <int MODE, int KW>
 void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                    hipStream_t s) {
     const int32_t chunk = 2 * KW * kRowThreads;
-    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->max_cols, 1), chunk);
+    const int32_t nchunks = (int32_t)ceil_div(std::max<int32_t>(c->cols_run, 1), chunk);
     const size_t lds = (size_t)KW * kRowThreads * sizeof(uint32_t);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     auto* rowptr = static_cast<const unsigned long long*>(c->rowptr.p);
     auto* recs = static_cast<const uint2*>(c->recs.p);
-    if (c->rows_kernel == RK_FUSED)
+    if (MODE == kModeFull || c->rows_kernel == RK_FUSED)
         hipLaunchKernelGGL((k_rows<MODE, KW, true>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    else
+    else if constexpr (MODE != kModeFull)  // work lists: the reference modes only
         hipLaunchKernelGGL((k_rows<MODE, KW, false>), dim3(re - rb, nchunks), dim3(kRowThreads), lds, s, c->dev, rb,
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
@@ -110,23 +110,33 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     case K: launch_pl<MODE, K, NT>(c, rb, re, flags, aji, S, N, s); break;
 #define KR_CASE(K) \
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
-    if (c->rows_kernel == RK_V2) {
-        switch (pick_kw<kV2Threads>(c->max_cols, 5)) {
-            case 1: launch_v2<MODE, 1>(c, rb, re, flags, aji, S, N, s); break;
-            case 2: launch_v2<MODE, 2>(c, rb, re, flags, aji, S, N, s); break;
-            case 3: launch_v2<MODE, 3>(c, rb, re, flags, aji, S, N, s); break;
-            case 4: launch_v2<MODE, 4>(c, rb, re, flags, aji, S, N, s); break;
-            default: launch_v2<MODE, 5>(c, rb, re, flags, aji, S, N, s); break;
+    if constexpr (MODE != kModeFull) {  // full rows: k_rows_pl / fused only
+        if (c->rows_kernel == RK_V2) {
+            switch (pick_kw<kV2Threads>(c->cols_run, 5)) {
+                case 1: launch_v2<MODE, 1>(c, rb, re, flags, aji, S, N, s); break;
+                case 2: launch_v2<MODE, 2>(c, rb, re, flags, aji, S, N, s); break;
+                case 3: launch_v2<MODE, 3>(c, rb, re, flags, aji, S, N, s); break;
+                case 4: launch_v2<MODE, 4>(c, rb, re, flags, aji, S, N, s); break;
+                default: launch_v2<MODE, 5>(c, rb, re, flags, aji, S, N, s); break;
+            }
+            return;
         }
-        return;
+        if (c->rows_kernel == RK_PL512) {
+            switch (pick_kw<512>(c->cols_run, 10)) {
+                PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
+                PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
+                default: break;
+            }
+            return;
+        }
     }
-    if (c->rows_kernel == RK_PL) {
+    if (c->rows_kernel == RK_PL || (MODE == kModeFull && c->rows_kernel != RK_FUSED)) {
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
-        const int kw = pick_kw<1024>(c->max_cols, km ? std::max(1, std::min(5, atoi(km))) : 5);
+        const int kw = pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 #ifdef PFAAI_DIAGNOSTICS
         if (MODE == 0 && kw == 5 && !c->windows && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
             const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
-            const int32_t nchunks = (int32_t)ceil_div((int64_t)c->max_cols + 1, chunk);
+            const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
             const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
             hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
@@ -154,14 +164,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             case 4: launch_pl<MODE, 4, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
             default: launch_pl<MODE, 5, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
         }
-    } else if (c->rows_kernel == RK_PL512) {
-        switch (pick_kw<512>(c->max_cols, 10)) {
-            PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
-            PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
-            default: break;
-        }
     } else {
-        switch (pick_kw<kRowThreads>(c->max_cols, 10)) {
+        switch (pick_kw<kRowThreads>(c->cols_run, 10)) {
             KR_CASE(1) KR_CASE(2) KR_CASE(3) KR_CASE(4) KR_CASE(5) KR_CASE(6) KR_CASE(8) KR_CASE(10)
             case 7: launch_k_rows<MODE, 8>(c, rb, re, flags, aji, S, N, s); break;
             case 9: launch_k_rows<MODE, 10>(c, rb, re, flags, aji, S, N, s); break;

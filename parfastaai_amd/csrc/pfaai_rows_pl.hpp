@@ -63,6 +63,7 @@ __device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint3
                                        int32_t whi) {
     if ((uint32_t)(b - wlo) >= (uint32_t)(whi - wlo)) return;  // also drops b = -1 (no member)
     if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
+    if (MODE == kModeFull && b == a) return;
     const uint32_t o = (uint32_t)(b - cc0);
     atomicAdd(&acc[o >> 1], 1u << ((o & 1u) << 4));
 }

@@ -62,6 +62,7 @@ __device__ __forceinline__ void v2_add(const Dev& d, int32_t a, int32_t b, int32
     const uint32_t o = (uint32_t)(b - wlo);
     if (o >= width) return;
     if (MODE == 1 && !(b != a && (!d.is_q[b] || b > a))) return;  // isValidPair, ds_impl.hpp:270-273
+    if (MODE == kModeFull && b == a) return;
     atomicAdd(acc_w + o, 1u);
 }
 

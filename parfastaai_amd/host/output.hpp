@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -85,48 +86,89 @@ std::vector<double> dense_matrix(const DS& ds, const std::vector<JAC>& jac, cons
                                  bool isSubset) {
     const int64_t nq = ds.qrySetSize(), nt = ds.tgtSetSize();
     std::vector<double> M((std::size_t)(nq * nt), 0.0);
+    if (!isSubset) {  // QT: the reference's ids (ref-compat) land off their row when nQ > nT: flat,
+                      // bounds-checked, and in JAC order there (later pairs overwrite, as main.cpp:149 does)
+#pragma omp parallel for schedule(static) if (nq <= nt)
+        for (int64_t i = 0; i < (int64_t)jac.size(); ++i) {
+            const int64_t f = (int64_t)ds.mapQueryId(jac[i].genomeA) * nt + ds.mapTargetId(jac[i].genomeB);
+            if (f >= 0 && f < nq * nt) M[(std::size_t)f] = aji[i];
+        }
+        return M;
+    }
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < (int64_t)jac.size(); ++i) {
         const int32_t a = jac[i].genomeA, b = jac[i].genomeB;
         M[(std::size_t)ds.mapQueryId(a) * nt + ds.mapTargetId(b)] = aji[i];
-        if (isSubset && ds.isQryGenome(b)) M[(std::size_t)ds.mapQueryId(b) * nt + ds.mapTargetId(a)] = aji[i];
+        if (ds.isQryGenome(b)) M[(std::size_t)ds.mapQueryId(b) * nt + ds.mapTargetId(a)] = aji[i];
     }
     return M;
 }
 
+// printOutput's CSV (main.cpp:156-174), written block of rows by block of
+// rows: header at open, then rows() any number of times in row order (every
+// OpenMP thread formats rows into its own buffer; they are written in order).
+class CsvWriter {
+  public:
+    CsvWriter(const std::string& path, const std::vector<std::string>& cols, const std::string& sep)
+        : m_f(std::fopen(path.c_str(), "w")), m_sep(sep), m_nc((int64_t)cols.size()) {
+        if (!m_f) return;
+        std::string head = sep;
+        for (std::size_t j = 0; j < cols.size(); ++j) {
+            if (j) head += sep;
+            head += cols[j];
+        }
+        head += '\n';
+        m_ok = std::fwrite(head.data(), 1, head.size(), m_f) == head.size();
+    }
+    ~CsvWriter() { close(); }
+    bool ok() const { return m_f && m_ok; }
+    // rows [r0, r1) named names[r], values M[(r - r0) * n_cols + c]
+    bool rows(const std::vector<std::string>& names, const double* M, int64_t r0, int64_t r1) {
+        if (!ok()) return false;
+        const int64_t block = 256;  // rows formatted per parallel batch, then written in order
+        for (int64_t b0 = r0; b0 < r1; b0 += block) {
+            const int64_t b1 = std::min(r1, b0 + block);
+            if ((int64_t)m_buf.size() < b1 - b0) m_buf.resize(b1 - b0);
+#pragma omp parallel for schedule(dynamic, 1)
+            for (int64_t r = b0; r < b1; ++r) {
+                std::string& s = m_buf[r - b0];
+                s.clear();
+                s.reserve(names[r].size() + m_nc * 20 + 2);
+                s += names[r];
+                s += m_sep;
+                char tmp[48];
+                const double* row = M + (std::size_t)(r - r0) * m_nc;
+                for (int64_t c = 0; c < m_nc; ++c) {
+                    if (c) s += m_sep;
+                    s.append(tmp, fmt_double(row[c], tmp));
+                }
+                s += '\n';
+            }
+            for (int64_t r = b0; r < b1; ++r)
+                m_ok = m_ok && std::fwrite(m_buf[r - b0].data(), 1, m_buf[r - b0].size(), m_f) == m_buf[r - b0].size();
+        }
+        return m_ok;
+    }
+    bool close() {
+        if (!m_f) return m_ok;
+        m_ok = std::fclose(m_f) == 0 && m_ok;
+        m_f = nullptr;
+        return m_ok;
+    }
+
+  private:
+    FILE* m_f;
+    std::string m_sep;
+    int64_t m_nc;
+    bool m_ok = false;
+    std::vector<std::string> m_buf;
+};
+
 inline int write_csv(const std::string& path, const std::vector<std::string>& rows,
                      const std::vector<std::string>& cols, const std::vector<double>& M, const std::string& sep) {
-    FILE* f = std::fopen(path.c_str(), "w");
-    if (!f) return 1;
-    std::string head = sep;
-    for (std::size_t j = 0; j < cols.size(); ++j) {
-        if (j) head += sep;
-        head += cols[j];
-    }
-    head += '\n';
-    std::fwrite(head.data(), 1, head.size(), f);
-    const int64_t nr = (int64_t)rows.size(), nc = (int64_t)cols.size();
-    const int64_t block = 256;  // rows formatted per parallel batch, then written in order
-    std::vector<std::string> buf(block);
-    for (int64_t r0 = 0; r0 < nr; r0 += block) {
-        const int64_t r1 = std::min(nr, r0 + block);
-#pragma omp parallel for schedule(dynamic, 1)
-        for (int64_t r = r0; r < r1; ++r) {
-            std::string& s = buf[r - r0];
-            s.clear();
-            s.reserve(rows[r].size() + nc * 20 + 2);
-            s += rows[r];
-            s += sep;
-            char tmp[48];
-            for (int64_t c = 0; c < nc; ++c) {
-                if (c) s += sep;
-                s.append(tmp, fmt_double(M[(std::size_t)r * nc + c], tmp));
-            }
-            s += '\n';
-        }
-        for (int64_t r = r0; r < r1; ++r) std::fwrite(buf[r - r0].data(), 1, buf[r - r0].size(), f);
-    }
-    return std::fclose(f) == 0 ? 0 : 1;
+    CsvWriter w(path, cols, sep);
+    w.rows(rows, M.data(), 0, (int64_t)rows.size());
+    return w.close() ? 0 : 1;
 }
 
 // cereal: std::vector<JACTuple<int,double>> (20-B packed records) / vector<double>

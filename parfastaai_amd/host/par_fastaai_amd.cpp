@@ -52,6 +52,8 @@ struct AppParams {  // main.cpp:56-131
     std::string dumpPrefix;    // --dump-arrays: write the loader's Lc/F/T (cereal) and exit (no GPU)
     std::string formatSelftest;  // --format-selftest FILE: print fmt-formatted doubles (hex input)
     std::string streamAji;       // --stream-aji FILE: pfaai_stream the AJI vector to FILE (no CSV)
+    bool streamCsv = false;      // --stream-csv: the CSV from streamed dense row tiles (no whole matrix)
+    long long tileRows = 0;      // --tile-rows N (0: ~256 MB tiles)
     long long tilePairs = 1ll << 27;
     std::vector<int> devices;    // --devices 0,1,...: one context per device, rows split (ALL / QT)
     bool loaderTetras = false;   // --loader tetras: F from `<p>_tetras` (else G from `<p>_genomes`)
@@ -104,7 +106,10 @@ const char* kUsage =
     "  --bin TEXT               Also write cereal binaries PREFIX_{jac,aji,aji_matrix}.bin\n"
     "  --stream-aji TEXT        Stream the AJI vector (JAC-index order, cereal vector<double>) to FILE\n"
     "                           tile by tile instead of writing the CSV matrix (-q not supported)\n"
-    "  --tile-pairs INT [134217728]  Pairs per streamed output tile\n";
+    "  --tile-pairs INT [134217728]  Pairs per streamed output tile\n"
+    "  --stream-csv             Write the CSV from streamed tiles of whole output rows (bounded memory;\n"
+    "                           same bytes as the default writer)\n"
+    "  --tile-rows INT          Rows per --stream-csv tile [about 256 MB of doubles]\n";
 
 // CLI11-compatible parse: returns -1 to continue, else the exit code.
 int parse(int argc, char** argv, AppParams& a) {
@@ -164,6 +169,13 @@ int parse(int argc, char** argv, AppParams& a) {
             a.loaderTetras = v == "tetras";
         } else if (is("--dump-genomes", "--dump-genomes")) {
             if (!value(a.dumpGenomes)) return 114;
+        } else if (s == "--stream-csv") {
+            a.streamCsv = true;
+        } else if (is("--tile-rows", "--tile-rows")) {
+            std::string v;
+            if (!value(v)) return 114;
+            a.tileRows = std::atoll(v.c_str());
+            if (a.tileRows < 1) return 105;
         } else if (is("--bin", "--bin")) {
             if (!value(a.binPrefix)) return 114;
         } else if (is("--dump-arrays", "--dump-arrays")) {
@@ -297,6 +309,31 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
             std::printf("AJI stream (MI355X) : %10.2f ms  (|E| = %lld) -> %s\n", ms_since(t0),
                         (long long)impl.nEvents(), app.streamAji.c_str());
             return rc;
+        }
+        if (app.streamCsv && !app.pathToOutputFile.empty()) {  // CSV from streamed dense row tiles
+            auto t1 = std::chrono::steady_clock::now();
+            std::printf("Writing output with %lld query genomes and %lld target genomes. \n",
+                        (long long)ds.qrySetSize(), (long long)ds.tgtSetSize());
+            CsvWriter w(app.pathToOutputFile, ds.refTargetSet(), app.outFieldSeparator);
+            if (!w.ok()) {
+                std::cerr << "Error in writing " << app.pathToOutputFile << std::endl;
+                return 1;
+            }
+            struct Ctx { CsvWriter* w; const std::vector<std::string>* names; };
+            Ctx cx{&w, &ds.refQuerySet()};
+            const int64_t ncols = (int64_t)ds.tgtSetSize();
+            const int64_t tr = app.tileRows > 0 ? app.tileRows : std::max<int64_t>(1, ((int64_t)1 << 25) / std::max<int64_t>(ncols, 1));
+            impl.streamMatrix(tr, [](void* u, int64_t r0, int64_t r1, int64_t, const double* block) -> int {
+                auto* x = static_cast<Ctx*>(u);
+                return x->w->rows(*x->names, block, r0, r1) ? 0 : PFAAI_RC_INVALID;
+            }, &cx);
+            if (!w.close()) {
+                std::cerr << "Error in writing " << app.pathToOutputFile << std::endl;
+                return 1;
+            }
+            std::printf("AJI + CSV (streamed): %10.2f ms  (%lld-row tiles; |E| both orientations = %lld)\n",
+                        ms_since(t1), (long long)tr, (long long)impl.nEvents());
+            return 0;
         }
         auto t1 = std::chrono::steady_clock::now();
         impl.run();

@@ -149,3 +149,78 @@ def test_cli_c1_rebuilt_db(tmp_path, compat):
     q.write_text(text("qsub_test_input.txt"))
     run(db, str(out), "-q", str(q), *compat)
     assert out.read_text() == text("qsub_test_output_matrix_wheader.csv")
+
+
+@pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
+def test_cli_stream_csv_bytes(tmp_path, name):
+    """--stream-csv (pfaai_stream_matrix tiles of 3 whole rows, formatted as
+    they arrive) writes the reference's CSV byte for byte."""
+    db = unpack(tmp_path, name + ".db")
+    out = tmp_path / "out.csv"
+    r = run(db, str(out), "--stream-csv", "--tile-rows", "3")
+    assert "CSV (streamed)" in r.stdout, r.stdout
+    assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
+
+
+@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12"])
+def test_cli_stream_csv_vs_reference_binary_on_syn(tmp_path, case):
+    import make_ref_vectors as mk
+    kind, kw = mk.CASES[case]
+    kw = dict(kw)
+    out = str(tmp_path / "out.csv")
+    s = ["--stream-csv", "--tile-rows", "5"]
+    if kind == "all":
+        db = str(tmp_path / "s.db")
+        syn.write_db(db, **kw)
+        run(db, out, *s)
+    elif kind == "qsub":
+        query = kw.pop("query")
+        db = str(tmp_path / "s.db")
+        g = syn.write_db(db, **kw)
+        ql = tmp_path / "q.txt"
+        ql.write_text("\n".join(g["genome_set"][i] for i in query) + "\n")
+        run(db, out, "-q", str(ql), *s)
+    else:
+        nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")
+        tdb, qdb = str(tmp_path / "t.db"), str(tmp_path / "q.db")
+        syn.write_db(tdb, n_genomes=nT, **kw)
+        syn.write_db(qdb, n_genomes=nQ, genome_prefix="qry", genome_seed=syn.DEFAULT_SEED + 1,
+                     n_clades=(nT + kw["clade_size"] - 1) // kw["clade_size"], clade_mod=True, **kw)
+        run(tdb, out, "-r", qdb, "--ref-compat", *s)
+    assert open(out).read() == text(f"ref_{case}.csv")
+
+
+def test_cli_stream_csv_c1_qsub(tmp_path):
+    from test_c1_loader import rebuild_xantho
+    db = rebuild_xantho(str(tmp_path))
+    q = tmp_path / "q.txt"
+    q.write_text(text("qsub_test_input.txt"))
+    out = tmp_path / "o.csv"
+    run(db, str(out), "-q", str(q), "--stream-csv", "--tile-rows", "2")
+    assert out.read_text() == text("qsub_test_output_matrix_wheader.csv")
+    run(db, str(out), "--stream-csv")
+    assert out.read_text() == text("xanthodb_aji_matrix_wheader.csv")
+
+
+def test_cli_stream_csv_40k_bounded_rss(tmp_path):
+    """40,000 genomes: the default writer holds the JAC vector (16 GB), the AJI
+    vector (6.4 GB) and the dense matrix (12.8 GB); --stream-csv holds the
+    loaded DB plus two 256 MB pinned tiles, so the CLI's peak RSS stays far
+    below any of them.  The CSV (~25 GB) goes to /dev/null; its bytes are
+    pinned by the fixture tests above (same code path)."""
+    import sys
+    db = str(tmp_path / "s40k.db")
+    syn.write_db(db, n_genomes=40000, n_prot=12, clade_size=40)
+    # peak RSS of the CLI alone: a fresh interpreter whose only child it is
+    probe = ("import resource, subprocess, sys\n"
+             "r = subprocess.run(sys.argv[1:], capture_output=True, text=True)\n"
+             "sys.stdout.write(r.stdout + r.stderr)\n"
+             "print('PEAK_KB', resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss)\n"
+             "sys.exit(r.returncode)\n")
+    r = subprocess.run([sys.executable, "-c", probe, CLI, db, "/dev/null", "--stream-csv"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "CSV (streamed)" in r.stdout, r.stdout
+    peak_kb = int(r.stdout.split("PEAK_KB")[1])
+    print(r.stdout)
+    assert peak_kb < 4_000_000, peak_kb  # < 4 GB, vs 35 GB for the default writer
