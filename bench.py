@@ -70,6 +70,41 @@ def traffic_from_profiles(genomes, prot, world):
         return None
 
 
+def host_info(threads):
+    """The CPU the baseline ran on: model name, logical CPUs of the machine,
+    CPUs this process may use (the box's cgroup share can be far smaller
+    than nproc), threads the baseline was given."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "threads_used": threads}
+
+
+def c2_reference():
+    """The reference's own end-to-end time at BASELINE config C2 (2,000
+    genomes, SQLite DB -> CSV), measured beside ours by tools/gpu/e2e_c2.py
+    and committed as profiles/r02_e2e_cli_c2.json."""
+    p = os.path.join(ROOT, "profiles", "r02_e2e_cli_c2.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return {"source": "profiles/r02_e2e_cli_c2.json", "genomes": d["genomes"],
+                "reference_wall_s": d["reference_wall_s"], "reference_threads": d["reference_threads"],
+                "ours_wall_s": d["ours_wall_s"], "csv_byte_identical": d["csv_byte_identical"]}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(sample_genomes=320, n_prot=100):
     """Reference CLI on a SYN sample; returns the cpu_baseline object."""
     from parfastaai_amd import syn
@@ -99,7 +134,8 @@ def cpu_baseline(sample_genomes=320, n_prot=100):
                     "sample": f"reference par_fastaai.x (built from its sources) on SYN N={sample_genomes} "
                               f"P={n_prot} all-vs-all; hot path = its own 'E constr. (fin)' + 'JAC "
                               f"Construction' timers = {hot_s:.2f} s (wall incl. SQLite+CSV {wall:.1f} s); "
-                              f"OMP_NUM_THREADS={threads}"}
+                              f"OMP_NUM_THREADS={threads}",
+                    "host": host_info(threads), "c2_end_to_end": c2_reference()}
     # fallback: the CPU oracle (single thread restatement of the reference)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -112,7 +148,7 @@ def cpu_baseline(sample_genomes=320, n_prot=100):
     dt = time.perf_counter() - t0
     return {"value": pairs / dt, "unit": "genome-pairs/s", "cores": 1, "kind": "port",
             "sample": f"CPU oracle (E build + radix sort + extents + JAC) on SYN N={sample_genomes} P={n_prot}, "
-                      f"{dt:.2f} s"}
+                      f"{dt:.2f} s", "host": host_info(1), "c2_end_to_end": c2_reference()}
 
 
 def main():

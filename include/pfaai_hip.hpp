@@ -87,6 +87,33 @@ void par_range(int64_t n, Fn fn) {
 }
 }  // namespace detail
 
+// Contiguous row blocks over `parts` devices: cut[0] = 0 .. cut[parts] = n,
+// balanced by the row-cost model of parfastaai_amd/shard.py:split_rows (the
+// same cuts, pinned by tests/test_integration_compile.py): all-vs-all row a
+// costs fixed + width = 0.75 n + (n - 1 - a); QT / QSUB rows are equal.
+inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
+    std::vector<int64_t> cut{0};
+    if (!all_vs_all) {
+        for (int r = 1; r < parts; ++r) cut.push_back(n * r / parts);
+        cut.push_back(n);
+        return cut;
+    }
+    const double k = 0.75 * (double)n;  // shard.FIXED_COST_FRACTION
+    auto before = [&](int64_t a) { return (double)a * k + (double)a * n - (double)(a * (a + 1) / 2); };
+    const double total = before(n);
+    for (int r = 1; r < parts; ++r) {
+        int64_t lo = cut.back(), hi = n;
+        const double target = total * r / parts;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (before(mid) < target) lo = mid + 1; else hi = mid;
+        }
+        cut.push_back(lo);
+    }
+    cut.push_back(n);
+    return cut;
+}
+
 // Mode of a DSIT (see the header comment); specialise for other types.
 // Works through the abstract DataStructInterface too (the reference's
 // PFDSInterface, main.cpp:48): a query-vs-target DSIT numbers its queries
@@ -245,30 +272,10 @@ class ParFAAIHipImpl {
   private:
     pfaai_ctx* ctx() const { return m_ctx.front().get(); }
 
-    // contiguous row blocks balanced by the row-cost model (shard.py:split_rows)
-    static std::vector<int64_t> splitRows(int64_t n, int parts, bool all_vs_all) {
-        std::vector<int64_t> cut{0};
-        const double k = 0.75 * (double)n;  // shard.FIXED_COST_FRACTION
-        auto before = [&](int64_t a) {
-            return all_vs_all ? (double)a * k + (double)a * n - (double)a * (a + 1) / 2.0 : (double)a;
-        };
-        const double total = before(n);
-        for (int r = 1; r < parts; ++r) {
-            int64_t lo = cut.back(), hi = n;
-            const double target = total * r / parts;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) / 2;
-                if (before(mid) < target) lo = mid + 1; else hi = mid;
-            }
-            cut.push_back(lo);
-        }
-        cut.push_back(n);
-        return cut;
-    }
     void computeMulti(uint32_t flags, double* S, int32_t* N) {
         int64_t rows = 0, pairs = 0;
         pfaai_shape(ctx(), &rows, &pairs);
-        const auto cut = splitRows(rows, (int)m_ctx.size(), m_mode == PFAAI_MODE_ALL);
+        const auto cut = split_rows(rows, (int)m_ctx.size(), m_mode == PFAAI_MODE_ALL);
         std::vector<int> rcs(m_ctx.size(), 0);
         std::vector<std::thread> th;
         for (std::size_t i = 0; i < m_ctx.size(); ++i)

@@ -70,6 +70,18 @@ __global__ void k_fp16(const int32_t* __restrict__ Fp, int64_t n, uint16_t* __re
 // (genome g, protein p, tetramer t) of G that is not in F is allowed only
 // where F has no run (t, p) at all (e.g. the -r path: G holds every tetramer
 // of both DBs, F only those in both, scp_db.hpp:459-466; such an entry meets
+
+// Words of a and b that differ, added to *ne (the both-given check when G and
+// the G built from F must be equal: a plain streaming compare).
+__global__ __launch_bounds__(256) void k_count_ne(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                  int64_t n, unsigned long long* __restrict__ ne) {
+    uint32_t k = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        k += a[i] != b[i];
+    k = wave_sum_u32_fwd(k);
+    if ((threadIdx.x & 63) == 0 && k) atomicAdd(ne, (unsigned long long)k);
+}
+
 // an empty run in the row kernels).  Binary search for (p, g) in F's
 // tetramer block, sorted by (protein, genome); *found counts the entries F
 // holds (== |F| when G covers F, lists being strictly ascending sets).  One

@@ -647,7 +647,33 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     ms_upload = ms(t1, t2);
     if (!in_f && (rc = build_f_from_g(c, ng, n_f, s))) return rc;
     bool has_g = in_g;
-    if (in_g && in_f && n_f) {  // both given: G must hold F's memberships (k_g_check)
+    if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
+        // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
+        // the transpose of F -- build that transpose (the F-only path) and
+        // compare word for word, a sort and a stream instead of a search per entry
+        DevBuf user_off, user_tet;
+        std::swap(user_off, c->G_off);
+        std::swap(user_tet, c->G_tet);
+        rc = build_g_from_f(c, ng, n_f, s);
+        auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+        unsigned long long ne = 0;
+        if (!rc) {
+            HIPCHK(c, hipMemsetAsync(sc + SC_GRAND, 0, sizeof(unsigned long long), s));
+            const int gb = (int)std::min<int64_t>(ceil_div(n_f, 256), 8192);
+            hipLaunchKernelGGL(k_count_ne, dim3(gb), dim3(256), 0, s, static_cast<const uint32_t*>(c->G_tet.p),
+                               static_cast<const uint32_t*>(user_tet.p), n_f, sc + SC_GRAND);
+            hipLaunchKernelGGL(k_count_ne, dim3((int)std::min<int64_t>(ceil_div(2 * (ng + 1), 256), 8192)), dim3(256), 0,
+                               s, static_cast<const uint32_t*>(c->G_off.p), static_cast<const uint32_t*>(user_off.p),
+                               2 * (ng + 1), sc + SC_GRAND);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipMemcpyAsync(&ne, sc + SC_GRAND, sizeof(ne), hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+        }
+        release(user_off);
+        release(user_tet);
+        if (rc) return rc;
+        if (ne) return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
+    } else if (in_g && in_f && n_f) {  // both given, G larger (QT: both DBs' lists): G must hold F (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
         int* err = reinterpret_cast<int*>(sc + SC_ERR);
         HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));

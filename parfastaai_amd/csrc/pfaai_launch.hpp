@@ -9,18 +9,18 @@
 
 namespace pfaai_impl {
 
-template <int MODE, int KW, int NT, int WPE = 4, bool NL = false>
+template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = false, int ABL = 0>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NL ? (size_t)KW * NT * 2 : 0);
+    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NK == 1 ? (size_t)KW * NT * 2 : 0);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #define PLK(BF)                                                                                                      \
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NL, BF>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, ABL>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, \
                        abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
         if (bigf) PLK(true); else PLK(false);
 #undef PLK
@@ -145,24 +145,37 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             return;
         }
 #endif
+#ifdef PFAAI_DIAGNOSTICS
+        // A/B of the N storage (NK) and S5 form (BR) at the benchmark shape
+        if (const char* v = DIAG_ENV("PFAAI_PL_VAR"); v && MODE == 0 && kw == 5 && c->prob.n_prot <= 255) {
+            const std::string sv(v);
+            if (sv == "nk0br") { launch_pl<MODE, 5, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk1br") { launch_pl<MODE, 5, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk2br") { launch_pl<MODE, 5, 1024, 8, 2, true>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk0") { launch_pl<MODE, 5, 1024, 8, 0, false>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk1") { launch_pl<MODE, 5, 1024, 8, 1, false>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk2") { launch_pl<MODE, 5, 1024, 8, 2, false>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "ABLATE_nodiv") { launch_pl<MODE, 5, 1024, 8, 1, true, 1>(c, rb, re, flags, aji, S, N, s); return; }
+        }
+#endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
         const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
         if (nl) {
             switch (kw) {
-                case 1: launch_pl<MODE, 1, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 2: launch_pl<MODE, 2, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 3: launch_pl<MODE, 3, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 4: launch_pl<MODE, 4, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
-                default: launch_pl<MODE, 5, 1024, 8, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 1: launch_pl<MODE, 1, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 2: launch_pl<MODE, 2, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 3: launch_pl<MODE, 3, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                case 4: launch_pl<MODE, 4, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                default: launch_pl<MODE, 5, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
             }
             return;
         }
         switch (kw) {
-            case 1: launch_pl<MODE, 1, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 2: launch_pl<MODE, 2, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 3: launch_pl<MODE, 3, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            case 4: launch_pl<MODE, 4, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
-            default: launch_pl<MODE, 5, 1024, 8>(c, rb, re, flags, aji, S, N, s); break;
+            case 1: launch_pl<MODE, 1, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
+            case 2: launch_pl<MODE, 2, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
+            case 3: launch_pl<MODE, 3, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
+            case 4: launch_pl<MODE, 4, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
+            default: launch_pl<MODE, 5, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
         }
     } else {
         switch (pick_kw<kRowThreads>(c->cols_run, 10)) {

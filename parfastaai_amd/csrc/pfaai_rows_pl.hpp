@@ -106,16 +106,19 @@ __device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, ui
 // tools/gpu/stage_clocks.py).
 constexpr int kClkBlocks = 256;
 
-// NL: the per-column counts N live in LDS (u8 pairs, P <= 255) instead of
-// registers -- 5 VGPRs less at KW = 5, paid for with half the task capacity.
+// NK: where the per-column counts N live.  0: u16 pairs in registers (KW
+// VGPRs, any P); 1: u8 pairs in LDS (P <= 255; no VGPRs, half the task
+// capacity, an LDS read-modify-write per word in S5); 2: u8 quads in
+// registers (P <= 255; ceil(KW / 2) VGPRs, two VALU ops per word:
+// N += pk_min(counter word, 1) shifted into place).
 // S5F: S5 (normalise protein i-1) runs FIRST in iteration i, on T words
 // loaded during iteration i-1.  At KW = 5 the 64-VGPR budget spills a few fp64
 // accumulators; their reloads in S5 are scratch loads, and gfx9 waits for
 // vector loads in order, so an S5 after the prefetches waited for the
 // members and run-table entries just issued (s_waitcnt vmcnt(0)) -- first, it
 // waits only for loads of the previous iteration, needed by now anyway.
-template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, bool NL = false, bool BIGF = false,
-          bool S5F = true>
+template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, int NK = 0, bool BIGF = false,
+          bool S5F = true, bool BR = false, int ABL = 0>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
                                                    uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
@@ -126,6 +129,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr int W = KW * NT;            // counter words per row chunk
     constexpr int EPT = kPlEntries / NT;  // G entries per thread
     constexpr int NG = NT / 4;            // 4-lane groups
+    constexpr bool NL = NK == 1;
+    constexpr int NN = NK == 0 ? KW : NK == 2 ? (KW + 1) / 2 : 1;  // N registers
     constexpr int TC = NL ? kPlTaskCap / 2 : kPlTaskCap;  // line tasks per stage
     extern __shared__ uint32_t pl_smem[];                // acc[2][W], goff[P + 1], (NL) n16[W]
     __shared__ uint2 rt[2][kPlEntries];                  // runs of a protein stage: member range [lo, hi)
@@ -165,11 +170,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const uint16_t* T16 = compat ? d.T16c : d.T16;
     const int64_t t16w = d.t16_cols >> 1;            // u32 words per protein row of T16
     double S[2 * KW];
-    uint32_t N[NL ? 1 : KW];  // packed u16 pair counts (registers unless NL)
+    uint32_t N[NN];  // NK 0: u16 pair of word k in N[k]; NK 2: word k's pair at bits 8(k&1) + {0, 16} of N[k/2]
 #pragma unroll
     for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; }
 #pragma unroll
-    for (int k = 0; k < (NL ? 1 : KW); ++k) N[k] = 0u;
+    for (int k = 0; k < NN; ++k) N[k] = 0u;
     uint32_t ev = 0;
     __syncthreads();
 
@@ -265,30 +270,60 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
     // S5 of protein i-1 on counter row (i-1)&1 with its T words (fp64,
     // ascending protein order per pair)
+    // d >= c always holds with the true T columns; only QT under REF_COMPAT
+    // (row Q: other genomes' T columns) can give d < c, d <= 0 -- that case
+    // keeps per-column branches and the IEEE fallback.  Otherwise S5 is
+    // branch-free per word: a zero counter divides 0 by max(d, 1) and adds an
+    // exact +0.0 (S >= +0), N adds pk_min(word, 1); only waves with no column
+    // in the chunk skip a word (a scalar branch, no exec-mask juggling).
+    auto n_add = [&](int k, uint32_t v, int32_t w) {
+        if constexpr (NK == 0) {
+            N[k] += min(v & 0xFFFFu, 1u) | (min(v >> 16, 1u) << 16);
+        } else if constexpr (NK == 2) {
+            N[k >> 1] += (min(v & 0xFFFFu, 1u) | (min(v >> 16, 1u) << 16)) << (8 * (k & 1));
+        } else {
+            n16[w] = (uint16_t)(n16[w] + min(v & 0xFFFFu, 1u) + (min(v >> 16, 1u) << 8));
+        }
+    };
     auto s5 = [&](int i, const uint32_t (&tw)[KW], int32_t ta) {
         if (!(i >= 1 && glen(i - 1) > 0u)) return;
         uint32_t* acc_p = acc + ((i - 1) & 1) * W;
+        const int32_t wbase = (int32_t)uni_u32((uint32_t)tid & ~63u);
+        if (BR || (MODE == 2 && compat)) {  // BR: per-column branches everywhere (A/B)
+            auto div = [&](int32_t c, int32_t dd) -> double {
+                if constexpr (ABL == 1) return (double)(c + dd);  // diagnostics: no division (wrong results)
+                if (MODE == 2 && compat) return exact_div_any((double)c, (double)dd);
+                return exact_div_small((double)c, (double)dd);
+            };
 #pragma unroll
-        for (int k = 0; k < KW; ++k) {
-            const int32_t w = tid + k * NT;
-            if (w < ncw) {
+            for (int k = 0; k < KW; ++k) {
+                const int32_t w = tid + k * NT;
                 const uint32_t v = acc_p[w];
                 if (v) {
                     acc_p[w] = 0u;
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     ev += (uint32_t)(c0 + c1);
-                    if constexpr (NL) n16[w] = (uint16_t)(n16[w] + (uint32_t)(c0 != 0) + ((uint32_t)(c1 != 0) << 8));
+                    n_add(k, v, w);
                     const int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
-                    if (c0) {
-                        S[2 * k] += exact_div_any((double)c0, (double)d0);
-                        if constexpr (!NL) N[k] += 1u;
-                    }
-                    if (c1) {
-                        S[2 * k + 1] += exact_div_any((double)c1, (double)d1);
-                        if constexpr (!NL) N[k] += 1u << 16;
-                    }
+                    if (c0) S[2 * k] += div(c0, d0);
+                    if (c1) S[2 * k + 1] += div(c1, d1);
                 }
             }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            if (wbase + k * NT >= ncw) break;  // wave-uniform: later words are further out
+            const int32_t w = tid + k * NT;
+            const uint32_t v = acc_p[w];
+            acc_p[w] = 0u;
+            const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
+            ev += (uint32_t)(c0 + c1);
+            n_add(k, v, w);
+            const int32_t d0 = max(ta + (int32_t)(tw[k] & 0xFFFFu) - c0, 1);
+            const int32_t d1 = max(ta + (int32_t)(tw[k] >> 16) - c1, 1);
+            S[2 * k] += exact_div_small((double)c0, (double)d0);
+            S[2 * k + 1] += exact_div_small((double)c1, (double)d1);
         }
     };
     uint32_t twc[KW];  // S5F: T words of the previous protein, carried across the barrier
@@ -391,7 +426,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             if (b < wlo || b >= whi || !col_valid<MODE>(d, a, b)) continue;
             const int64_t idx = pair_index<MODE>(d, a, b, compat);
             double s = S[2 * k + h];
-            int32_t n = NL ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu) : (int32_t)((N[NL ? 0 : k] >> (16 * h)) & 0xFFFFu);
+            int32_t n = NK == 1 ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu)
+                        : NK == 2 ? (int32_t)((N[(k >> 1) % NN] >> (8 * (k & 1) + 16 * h)) & 0xFFu)
+                                  : (int32_t)((N[k % NN] >> (16 * h)) & 0xFFFFu);
             if (n == 0 && compat) {
                 // extents stay 0/0 -> J of E[0]'s protein, N = 1
                 const unsigned long long key = *first_key;
