@@ -9,7 +9,7 @@
 
 namespace pfaai_impl {
 
-template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = false, int ABL = 0>
+template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = false, int VAR = 0>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
@@ -18,11 +18,19 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    // member window test (k_rows_pl WK): one chunk per row reaches the last
+    // id, so all-vs-all rows test only b > a and -q / full rows test nothing
+    constexpr int kWk1 = MODE == 0 ? 1 : MODE == 2 ? 0 : 2;
+    const int wk = nchunks == 1 && !DIAG_ENV("PFAAI_PL_WK0") ? kWk1 : 0;
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
-#define PLK(BF)                                                                                                      \
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, ABL>), dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, \
-                       abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
-        if (bigf) PLK(true); else PLK(false);
+#define PLK(BF, WKV)                                                                                                 \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, WKV>), dim3(r1 - r0, gy), dim3(NT), lds, \
+                       s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+        if (wk == 0 || abs_chunk >= 0) {
+            if (bigf) PLK(true, 0); else PLK(false, 0);
+        } else if constexpr (kWk1 != 0) {
+            if (bigf) PLK(true, kWk1); else PLK(false, kWk1);
+        }
 #undef PLK
     };
     if (nchunks == 1 || !c->windows) {
@@ -134,12 +142,13 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 #ifdef PFAAI_DIAGNOSTICS
-        if (MODE == 0 && kw == 5 && !c->windows && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+        if (MODE == 0 && kw == 5 && !c->windows && c->prob.n_prot <= 255 && DIAG_ENV("PFAAI_PL_CLK") &&
+            c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
             const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t);
+            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t) + 5 * 1024 * 2;
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
+            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, true, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
                                chunk, -1, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
                                static_cast<unsigned long long*>(c->dbg.p));
             return;
@@ -156,6 +165,9 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "nk1") { launch_pl<MODE, 5, 1024, 8, 1, false>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "nk2") { launch_pl<MODE, 5, 1024, 8, 2, false>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "ABLATE_nodiv") { launch_pl<MODE, 5, 1024, 8, 1, true, 1>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk1br_v2") { launch_pl<MODE, 5, 1024, 8, 1, true, 2>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk1br_v4") { launch_pl<MODE, 5, 1024, 8, 1, true, 4>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "nk1br_v6") { launch_pl<MODE, 5, 1024, 8, 1, true, 6>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

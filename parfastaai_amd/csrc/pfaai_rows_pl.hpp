@@ -47,6 +47,8 @@
 // every (genome, protein) G list <= kPlEntries entries, ncw <= KW*NT
 // counter words per chunk, T < 2^16.
 #pragma once
+#include <type_traits>
+
 #include "pfaai_util.hpp"
 
 namespace pfaai {
@@ -100,6 +102,55 @@ __device__ __forceinline__ void pl_scatter4(const Dev& d, int32_t a, uint4 b, ui
     pl_add<MODE>(d, a, (ok & 8u) ? (int32_t)b.w : -1, acc, cc0, wlo, whi);
 }
 
+// The same three steps with fewer VALU operations (the kernel is VALU-bound:
+// ~85 % of a SIMD's issue cycles at 10k, rocprofv3 SQ_INSTS_VALU):
+//  * pl_issue_m: the task's valid members form the contiguous range
+//    [lo, hi) of the lane's 4 (run bounds minus the lane's first member
+//    index), so the 4-bit mask is one bit-field (v_med3 clamps + v_bfm)
+//    instead of eight compares;
+//  * pl_add_m: chunks start at even columns, so counter word (b - cc0) / 2
+//    is accb[b >> 1] with accb = acc - cc0 / 2, and the member's mask bit
+//    joins the window test in one predicate.
+template <int TC = kPlTaskCap, bool BIGF = false>
+__device__ __forceinline__ uint32_t pl_issue_m(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
+                                               const uint2* rt, int k, int nt, uint32_t gl4, uint4& b) {
+    const uint32_t t = tk[min(k, TC - 1)];
+    const uint2 rr = rt[t & 1023u];
+    const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + ((t >> 6) & ~15u) + gl4;  // + (t >> 10) * 16
+    const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 4);
+    const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 4);
+    uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
+    if (!(k < nt && t != kPlNoTask)) mask = 0u;
+    if constexpr (BIGF)
+        b = *reinterpret_cast<const uint4*>(Fg + (mask ? m0 : 0u));
+    else
+        b = bld_u128(fg, mask ? m0 * 4u : kOOB, 0u);
+    return mask;
+}
+
+// WK: the window test a member needs -- 0: wlo <= b < whi; 1: wlo <= b (the
+// window reaches the last id, e.g. an all-vs-all row in one chunk); 2: none
+// (the window is every id, e.g. a full row).
+template <int MODE, int WK>
+__device__ __forceinline__ void pl_add_m(const Dev& d, int32_t a, int32_t b, bool valid, uint32_t* accb, int32_t wlo,
+                                         uint32_t wspan) {
+    bool ok = valid;
+    if constexpr (WK == 0) ok = ok && (uint32_t)(b - wlo) < wspan;
+    if constexpr (WK == 1) ok = ok && b >= wlo;
+    if (MODE == 1) ok = ok && b != a && (!d.is_q[b] || b > a);  // isValidPair, ds_impl.hpp:270-273
+    if (MODE == kModeFull) ok = ok && b != a;
+    if (ok) atomicAdd(&accb[(uint32_t)b >> 1], 1u << (((uint32_t)b & 1u) << 4));
+}
+
+template <int MODE, int WK>
+__device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, uint32_t m, uint32_t* accb,
+                                              int32_t wlo, uint32_t wspan) {
+    pl_add_m<MODE, WK>(d, a, (int32_t)b.x, m & 1u, accb, wlo, wspan);
+    pl_add_m<MODE, WK>(d, a, (int32_t)b.y, m & 2u, accb, wlo, wspan);
+    pl_add_m<MODE, WK>(d, a, (int32_t)b.z, m & 4u, accb, wlo, wspan);
+    pl_add_m<MODE, WK>(d, a, (int32_t)b.w, m & 8u, accb, wlo, wspan);
+}
+
 // CLK (diagnostics, PFAAI_PL_CLK): every wave of the first kClkBlocks
 // workgroups sums the shader-clock time of each stage of the protein loop
 // into clk[(block * (NT / 64) + wave) * 8 + stage] (pfaai_debug_clocks,
@@ -118,7 +169,7 @@ constexpr int kClkBlocks = 256;
 // members and run-table entries just issued (s_waitcnt vmcnt(0)) -- first, it
 // waits only for loads of the previous iteration, needed by now anyway.
 template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, int NK = 0, bool BIGF = false,
-          bool S5F = true, bool BR = false, int ABL = 0>
+          bool S5F = true, bool BR = false, int VAR = 0, int WK = 0>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
                                                    uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
@@ -282,7 +333,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         } else if constexpr (NK == 2) {
             N[k >> 1] += (min(v & 0xFFFFu, 1u) | (min(v >> 16, 1u) << 16)) << (8 * (k & 1));
         } else {
-            n16[w] = (uint16_t)(n16[w] + min(v & 0xFFFFu, 1u) + (min(v >> 16, 1u) << 8));
+            if constexpr ((VAR & 4) != 0)  // first form (A/B)
+                n16[w] = (uint16_t)(n16[w] + (uint32_t)((v & 0xFFFFu) != 0u) + ((uint32_t)((v >> 16) != 0u) << 8));
+            else
+                n16[w] = (uint16_t)(n16[w] + min(v & 0xFFFFu, 1u) + (min(v >> 16, 1u) << 8));
         }
     };
     auto s5 = [&](int i, const uint32_t (&tw)[KW], int32_t ta) {
@@ -291,7 +345,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         const int32_t wbase = (int32_t)uni_u32((uint32_t)tid & ~63u);
         if (BR || (MODE == 2 && compat)) {  // BR: per-column branches everywhere (A/B)
             auto div = [&](int32_t c, int32_t dd) -> double {
-                if constexpr (ABL == 1) return (double)(c + dd);  // diagnostics: no division (wrong results)
+                if constexpr ((VAR & 1) != 0) return (double)(c + dd);  // diagnostics: no division (wrong results)
                 if (MODE == 2 && compat) return exact_div_any((double)c, (double)dd);
                 return exact_div_small((double)c, (double)dd);
             };
@@ -330,13 +384,31 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
     int32_t tac = 0;
+    // member path: VAR bit 2 keeps the first form (pl_issue / pl_scatter4) for A/B
+    constexpr bool kLegacyM = (VAR & 2) != 0;
+    const uint32_t gl4 = 4u * (uint32_t)gl, wspan = (uint32_t)(whi - wlo);
+    int st_cur = 0;
+    auto issue = [&](int k, int ntk, uint4& bb) -> uint32_t {
+        if constexpr (kLegacyM) return pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl, bb);
+        return pl_issue_m<TC, BIGF>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl4, bb);
+    };
+    // WK: the window test of pl_add_m, chosen by the launcher for every row
+    // of the launch (pfaai_launch.hpp)
+    auto scatter = [&](uint32_t* acc_x, uint4 bb, uint32_t m) {
+        if constexpr (kLegacyM) pl_scatter4<MODE>(d, a, bb, m, acc_x, cc0, wlo, whi);
+        else pl_scatter4_m<MODE, WK>(d, a, bb, m, acc_x - (cc0 >> 1), wlo, wspan);
+    };
 
 #pragma unroll 1
     for (int i = 0; i <= P; ++i) {
         const int st = i & 1, cs = i % 3;
+        st_cur = st;
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
-        if constexpr (S5F) s5(i, twc, tac);
+        if constexpr (S5F) {
+            s5(i, twc, tac);
+            stamp(7);
+        }
         // T words of the thread's columns and T[p][A] (S5F: of protein i, for
         // the next iteration; else of protein i-1, issued first so that S5
         // waits for nothing issued after them)
@@ -350,7 +422,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // S4a: first round of member loads of protein i (one task per 4-lane group)
         const int nt = has_i ? min((int)uni_u32(ntask[cs]), TC) : 0;
         uint4 b;
-        uint32_t okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], grp, nt, gl, b);
+        uint32_t okm = issue(grp, nt, b);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
         if (i + 1 < P) s3(i + 1, r4);
@@ -372,19 +444,19 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // S4b: atomics of the first round, further rounds (two tasks per
         // group in flight), whole-workgroup runs
         if (has_i) {
-            pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
+            scatter(acc_i, b, okm);
             stamp(4);
             int k = grp + NG;
             for (; k + NG < nt; k += 2 * NG) {
                 uint4 b2;
-                okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k, nt, gl, b);
-                const uint32_t ok2 = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k + NG, nt, gl, b2);
-                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
-                pl_scatter4<MODE>(d, a, b2, ok2, acc_i, cc0, wlo, whi);
+                okm = issue(k, nt, b);
+                const uint32_t ok2 = issue(k + NG, nt, b2);
+                scatter(acc_i, b, okm);
+                scatter(acc_i, b2, ok2);
             }
             if (k < nt) {
-                okm = pl_issue<TC, BIGF>(r_fg, d.Fg, tk[st], rt[st], k, nt, gl, b);
-                pl_scatter4<MODE>(d, a, b, okm, acc_i, cc0, wlo, whi);
+                okm = issue(k, nt, b);
+                scatter(acc_i, b, okm);
             }
             if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
                 for (int wd = 0; wd < kPlEntries / 32; ++wd) {
@@ -408,7 +480,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     }
     if constexpr (CLK) {
         if (lane == 0 && blockIdx.x < kClkBlocks && blockIdx.y == 0)
-            for (int j = 0; j < 7; ++j) clk[((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 8 + j] = ck[j];
+            for (int j = 0; j < 8; ++j) clk[((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 8 + j] = ck[j];
     }
 
     // |E| of this row chunk (the sum of its counters over all proteins)

@@ -46,11 +46,12 @@ if a.v2:
     names = ["T issue + S3", "M/S2/S1 issue", "S5 normalise", "S4 prefetched", "S4 further rounds", "long runs",
              "barrier"]
 else:
-    names = ["T + S4a issue", "S3 tasks", "S2/S1 issue", "S5 normalise", "S4b round 1", "S4b rounds 2+/whole",
-             "recycle+barrier"]
-used = c[:, 0, :7].sum(axis=1) > 0
+    names = ["T + S4a issue", "S3 tasks", "S2/S1 issue", "T-word carry", "S4b round 1", "S4b rounds 2+/whole",
+             "recycle+barrier", "S5 normalise (first)"]
+K = len(names)
+used = c[:, 0, :K].sum(axis=1) > 0
 c = c[used]
-tot = c[:, :, :7].sum(axis=2)
+tot = c[:, :, :K].sum(axis=2)
 print(f"{'k_rows_v2' if a.v2 else 'k_rows_pl'} rows [{r0}, {r1}): {r_plain:.3f} ms plain, {r:.3f} ms clock variant; "
       f"{used.sum()} workgroups sampled; per wave-loop total: median {np.median(tot):.0f} cycles")
 for j, nm in enumerate(names):

@@ -9,10 +9,13 @@
 #ifndef S5FP
 #define S5FP true
 #endif
+#ifndef WKP
+#define WKP 1
+#endif
 #ifndef BRP
 #define BRP true
 #endif
 
-template __global__ void pfaai::k_rows_pl<0, 5, 1024, 8, false, NKP, false, S5FP, BRP>(
+template __global__ void pfaai::k_rows_pl<0, 5, 1024, 8, false, NKP, false, S5FP, BRP, 0, WKP>(
     pfaai::Dev, int64_t, int32_t, int32_t, uint32_t, const unsigned long long*, double*, double*, int32_t*,
     unsigned long long*, unsigned long long*);
