@@ -253,7 +253,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
                      !(wv && wv[0] == '0') &&
                      (int64_t)c->max_cols + 1 > wcols;
-        if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 64 KB of LDS
+        if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 80 KB of LDS (nwin * P <= 5120)
             nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
             win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * (int64_t)c->prob.n_prot * nwin));
             c->windows = win_tile >= 1 &&
@@ -269,7 +269,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         if (!keep) {
             Dev dw = c->dev;
             dw.blk = static_cast<uint4*>(c->blkw.p);
-            // 1024 threads: the 64 KB of LDS staging allows two workgroups per
+            // 1024 threads: the 80 KB of LDS staging allows two workgroups per
             // CU, so a 256-thread form ran 8 waves per CU (PFAAI_BLK_THREADS=256
             // A/B: 6.0 -> 2.9 ms at QT 50 000 x 1 000)
             const size_t lds = (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4);

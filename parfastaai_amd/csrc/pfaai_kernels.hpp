@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 //             holding A, i.e. its E triples (ds_helper.hpp:270-357).
 // ---------------------------------------------------------------------------
 constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer for many proteins)
-constexpr int kBlkLdsBytes = 64 << 10;  // its LDS staging: n_prot x tile x 16 B
+constexpr int kBlkLdsBytes = 80 << 10;  // its LDS staging: n_prot x tile x 16 B (two workgroups share a CU's 160 KB)
 
 // dbg (diagnostics, PFAAI_BLK_ABLATE): bit 0 skips (1), bit 1 (2), bit 2 (3).
 // WIN (column windows for rows wider than one row-kernel chunk): one table

@@ -151,6 +151,29 @@ __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, 
     pl_add_m<MODE, WK>(d, a, (int32_t)b.w, m & 8u, accb, wlo, wspan);
 }
 
+// Two-lane groups (k_rows_pl VAR bit 8): a lane takes half a line task, 8
+// members by two 16-B loads, so a protein's tasks fill half as many wave
+// rounds and the per-task issue work is shared by 8 members instead of 4.
+template <int TC = kPlTaskCap, bool BIGF = false>
+__device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
+                                                const uint2* rt, int k, int nt, uint32_t gl8, uint4& b, uint4& bh) {
+    const uint32_t t = tk[min(k, TC - 1)];
+    const uint2 rr = rt[t & 1023u];
+    const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + ((t >> 6) & ~15u) + gl8;
+    const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 8);
+    const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 8);
+    uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
+    if (!(k < nt && t != kPlNoTask)) mask = 0u;
+    if constexpr (BIGF) {
+        b = *reinterpret_cast<const uint4*>(Fg + ((mask & 15u) ? m0 : 0u));
+        bh = *reinterpret_cast<const uint4*>(Fg + ((mask >> 4) ? m0 + 4u : 0u));
+    } else {
+        b = bld_u128(fg, (mask & 15u) ? m0 * 4u : kOOB, 0u);
+        bh = bld_u128(fg, (mask >> 4) ? m0 * 4u + 16u : kOOB, 0u);
+    }
+    return mask;
+}
+
 // CLK (diagnostics, PFAAI_PL_CLK): every wave of the first kClkBlocks
 // workgroups sums the shader-clock time of each stage of the protein loop
 // into clk[(block * (NT / 64) + wave) * 8 + stage] (pfaai_debug_clocks,
@@ -384,8 +407,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
     int32_t tac = 0;
-    // member path: VAR bit 2 keeps the first form (pl_issue / pl_scatter4) for A/B
+    // member path: VAR bit 2 keeps the first form (pl_issue / pl_scatter4) for A/B;
+    // VAR bit 8: two-lane groups (pl_issue_m2), 8 members per lane and task
     constexpr bool kLegacyM = (VAR & 2) != 0;
+    constexpr bool G2 = (VAR & 8) != 0 && !kLegacyM;
+    constexpr int NGX = G2 ? NT / 2 : NG;
+    const int grpx = G2 ? tid >> 1 : grp;
+    const uint32_t gl8 = 8u * (uint32_t)(tid & 1);
     const uint32_t gl4 = 4u * (uint32_t)gl, wspan = (uint32_t)(whi - wlo);
     int st_cur = 0;
     auto issue = [&](int k, int ntk, uint4& bb) -> uint32_t {
@@ -397,6 +425,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     auto scatter = [&](uint32_t* acc_x, uint4 bb, uint32_t m) {
         if constexpr (kLegacyM) pl_scatter4<MODE>(d, a, bb, m, acc_x, cc0, wlo, whi);
         else pl_scatter4_m<MODE, WK>(d, a, bb, m, acc_x - (cc0 >> 1), wlo, wspan);
+    };
+    auto issue2 = [&](int k, int ntk, uint4& bb, uint4& bbh) -> uint32_t {
+        return pl_issue_m2<TC, BIGF>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
+    };
+    auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
+        pl_scatter4_m<MODE, WK>(d, a, bb, m & 15u, acc_x - (cc0 >> 1), wlo, wspan);
+        pl_scatter4_m<MODE, WK>(d, a, bbh, m >> 4, acc_x - (cc0 >> 1), wlo, wspan);
     };
 
 #pragma unroll 1
@@ -421,8 +456,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
         // S4a: first round of member loads of protein i (one task per 4-lane group)
         const int nt = has_i ? min((int)uni_u32(ntask[cs]), TC) : 0;
-        uint4 b;
-        uint32_t okm = issue(grp, nt, b);
+        uint4 b, bh;
+        uint32_t okm = G2 ? issue2(grpx, nt, b, bh) : issue(grp, nt, b);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
         if (i + 1 < P) s3(i + 1, r4);
@@ -437,26 +472,35 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         } else {
 #pragma unroll
             for (int k = 0; k < KW; ++k) twc[k] = tw[k];
-            tac = ta;
+            tac = (int32_t)uni_u32((uint32_t)ta);  // uniform: an SGPR across the barrier
         }
         stamp(3);
         if (prio & 2u) __builtin_amdgcn_s_setprio(1);
         // S4b: atomics of the first round, further rounds (two tasks per
         // group in flight), whole-workgroup runs
         if (has_i) {
-            scatter(acc_i, b, okm);
-            stamp(4);
-            int k = grp + NG;
-            for (; k + NG < nt; k += 2 * NG) {
-                uint4 b2;
-                okm = issue(k, nt, b);
-                const uint32_t ok2 = issue(k + NG, nt, b2);
+            if constexpr (G2) {
+                scatter8(acc_i, b, bh, okm);
+                stamp(4);
+                for (int k = grpx + NGX; k < nt; k += NGX) {
+                    okm = issue2(k, nt, b, bh);
+                    scatter8(acc_i, b, bh, okm);
+                }
+            } else {
                 scatter(acc_i, b, okm);
-                scatter(acc_i, b2, ok2);
-            }
-            if (k < nt) {
-                okm = issue(k, nt, b);
-                scatter(acc_i, b, okm);
+                stamp(4);
+                int k = grp + NG;
+                for (; k + NG < nt; k += 2 * NG) {
+                    uint4 b2;
+                    okm = issue(k, nt, b);
+                    const uint32_t ok2 = issue(k + NG, nt, b2);
+                    scatter(acc_i, b, okm);
+                    scatter(acc_i, b2, ok2);
+                }
+                if (k < nt) {
+                    okm = issue(k, nt, b);
+                    scatter(acc_i, b, okm);
+                }
             }
             if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
                 for (int wd = 0; wd < kPlEntries / 32; ++wd) {

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--workdir", default="/tmp/pfaai_e2e")
     ap.add_argument("--ref-timeout", type=int, default=600)
+    ap.add_argument("--ours-args", default="", help="extra par_fastaai_amd options, e.g. --stream-csv")
+    ap.add_argument("--ref-csv", default=None, help="compare with this reference CSV instead of running the reference")
     a = ap.parse_args()
     from parfastaai_amd import syn
 
@@ -55,17 +57,21 @@ def main():
         return w, [l.strip() for l in out.splitlines() if ":" in l and ("ms" in l or "time" in l.lower())]
 
     ours_csv, ref_csv = os.path.join(a.workdir, "ours.csv"), os.path.join(a.workdir, "ref.csv")
-    w_ours, l_ours = run([os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd"), db, ours_csv])
+    w_ours, l_ours = run([os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd"), db, ours_csv,
+                          *a.ours_args.split()])
     print(f"[e2e] ours {w_ours:.2f}s", file=sys.stderr, flush=True)
     env = dict(os.environ, OMP_NUM_THREADS="16")
-    w_ref, l_ref = run([os.path.join(ROOT, "oracle", "_ref", "par_fastaai.x"), db, ref_csv], env, a.ref_timeout)
-    print(f"[e2e] reference {w_ref:.2f}s", file=sys.stderr, flush=True)
+    if a.ref_csv:  # an earlier reference run of the same DB
+        ref_csv, w_ref, l_ref = a.ref_csv, float("nan"), []
+    else:
+        w_ref, l_ref = run([os.path.join(ROOT, "oracle", "_ref", "par_fastaai.x"), db, ref_csv], env, a.ref_timeout)
+        print(f"[e2e] reference {w_ref:.2f}s", file=sys.stderr, flush=True)
     same = open(ours_csv, "rb").read() == open(ref_csv, "rb").read()
     pairs = a.genomes * (a.genomes - 1) // 2
     print(json.dumps({
         "what": "end-to-end CLI, SQLite DB -> CSV (BASELINE config C2 shape)",
         "genomes": a.genomes, "proteins": a.prot, "pairs": pairs,
-        "ours_wall_s": round(w_ours, 2), "ours_phases": l_ours,
+        "ours_wall_s": round(w_ours, 2), "ours_args": a.ours_args, "ours_phases": l_ours,
         "reference_wall_s": round(w_ref, 2), "reference_threads": 16, "reference_phases": l_ref,
         "speedup_wall": round(w_ref / w_ours, 1), "csv_byte_identical": same,
         "csv_bytes": os.path.getsize(ours_csv),

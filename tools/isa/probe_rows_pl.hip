@@ -9,6 +9,9 @@
 #ifndef S5FP
 #define S5FP true
 #endif
+#ifndef VARP
+#define VARP 0
+#endif
 #ifndef WKP
 #define WKP 1
 #endif
@@ -16,6 +19,6 @@
 #define BRP true
 #endif
 
-template __global__ void pfaai::k_rows_pl<0, 5, 1024, 8, false, NKP, false, S5FP, BRP, 0, WKP>(
+template __global__ void pfaai::k_rows_pl<0, 5, 1024, 8, false, NKP, false, S5FP, BRP, VARP, WKP>(
     pfaai::Dev, int64_t, int32_t, int32_t, uint32_t, const unsigned long long*, double*, double*, int32_t*,
     unsigned long long*, unsigned long long*);
