@@ -9,7 +9,7 @@
 
 namespace pfaai_impl {
 
-template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = false, int VAR = 0>
+template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = true, int VAR = 0>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
@@ -168,7 +168,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "nk1br_v2") { launch_pl<MODE, 5, 1024, 8, 1, true, 2>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "nk1br_v4") { launch_pl<MODE, 5, 1024, 8, 1, true, 4>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "nk1br_v6") { launch_pl<MODE, 5, 1024, 8, 1, true, 6>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "g2") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "g4") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

@@ -151,7 +151,7 @@ __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, 
     pl_add_m<MODE, WK>(d, a, (int32_t)b.w, m & 8u, accb, wlo, wspan);
 }
 
-// Two-lane groups (k_rows_pl VAR bit 8): a lane takes half a line task, 8
+// Two-lane groups (the k_rows_pl default): a lane takes half a line task, 8
 // members by two 16-B loads, so a protein's tasks fill half as many wave
 // rounds and the per-task issue work is shared by 8 members instead of 4.
 template <int TC = kPlTaskCap, bool BIGF = false>
@@ -407,10 +407,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
     int32_t tac = 0;
-    // member path: VAR bit 2 keeps the first form (pl_issue / pl_scatter4) for A/B;
-    // VAR bit 8: two-lane groups (pl_issue_m2), 8 members per lane and task
+    // member path: two-lane groups (pl_issue_m2), 8 members per lane and task
+    // (10.60 -> 10.47 ms, VALU instructions -5.8 % at 10k); VAR bit 8 keeps the
+    // four-lane groups with two tasks in flight, VAR bit 2 the first form
+    // (pl_issue / pl_scatter4), for A/B
     constexpr bool kLegacyM = (VAR & 2) != 0;
-    constexpr bool G2 = (VAR & 8) != 0 && !kLegacyM;
+    constexpr bool G2 = (VAR & 8) == 0 && !kLegacyM;
     constexpr int NGX = G2 ? NT / 2 : NG;
     const int grpx = G2 ? tid >> 1 : grp;
     const uint32_t gl8 = 8u * (uint32_t)(tid & 1);
