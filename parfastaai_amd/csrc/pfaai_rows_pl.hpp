@@ -232,6 +232,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
     uint16_t* n16 = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1);  // NL: N of columns (2w, 2w+1) as u8 pair
+    uint16_t* taL = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1 + (NL ? W / 2 : 0));  // T[p][A], p < P
 
     const int64_t g0 = d.G_off[(int64_t)a * P];
     for (int p = tid; p <= P; p += NT) goff[p] = (uint32_t)(d.G_off[(int64_t)a * P + p] - g0);
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     if (tid < 3) { ntask[tid] = 0u; nwhole[tid] = 0u; }
     for (int w = tid; w < 3 * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
     const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
+    for (int p = tid; p < P; p += NT) taL[p] = (uint16_t)d.T[(int64_t)p * d.t_cols + tca];
     const uint16_t* T16 = compat ? d.T16c : d.T16;
     const int64_t t16w = d.t16_cols >> 1;            // u32 words per protein row of T16
     double S[2 * KW];
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
             for (int k = 0; k < KW; ++k) {
                 const int32_t w = tid + k * NT;
-                const uint32_t v = acc_p[w];
+                const uint32_t v = acc_p[w];  // (a wave-uniform skip past ncw measured 2 % slower)
                 if (v) {
                     acc_p[w] = 0u;
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
@@ -407,6 +409,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
     int32_t tac = 0;
+    // TL (default; VAR bit 32 restores the first form for A/B): the T words
+    // are loaded after S4b instead of before S4a, so they are live across the
+    // barrier only, not across the member rounds, and T[p][A] comes from an
+    // LDS table filled once per row -- one spilled fp64 accumulator instead of
+    // two, 10.37 -> 10.10 ms at 10k
+    constexpr bool TL = S5F && (VAR & 32) == 0;
     // member path: two-lane groups (pl_issue_m2), 8 members per lane and task
     // (10.60 -> 10.47 ms, VALU instructions -5.8 % at 10k); VAR bit 8 keeps the
     // four-lane groups with two tasks in flight, VAR bit 2 the first form
@@ -443,7 +451,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
         if constexpr (S5F) {
-            s5(i, twc, tac);
+            s5(i, twc, TL ? (i >= 1 ? (int32_t)uni_u32(taL[i - 1]) : 0) : tac);
             stamp(7);
         }
         // T words of the thread's columns and T[p][A] (S5F: of protein i, for
@@ -452,10 +460,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         const int pt = S5F ? min(i, P - 1) : (i >= 1 ? i - 1 : 0);
         if (prio & 1u) __builtin_amdgcn_s_setprio(2);  // loads issue ahead of other waves' S5 (flags bits 16-17)
         uint32_t tw[KW];
+        int32_t ta = 0;
         const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
+        const uint32_t tao = (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u;
+        if constexpr (!TL) {
 #pragma unroll
-        for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
-        const int32_t ta = (int32_t)bld_u32(r_t, 0u, (uint32_t)((int64_t)pt * d.t_cols + tca) * 4u);
+            for (int k = 0; k < KW; ++k) tw[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
+            ta = (int32_t)bld_u32(r_t, 0u, tao);
+        }
         // S4a: first round of member loads of protein i (one task per 4-lane group)
         const int nt = has_i ? min((int)uni_u32(ntask[cs]), TC) : 0;
         uint4 b, bh;
@@ -471,7 +483,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // S5: normalise protein i-1
         if constexpr (!S5F) {
             s5(i, tw, ta);
-        } else {
+        } else if constexpr (!TL) {
 #pragma unroll
             for (int k = 0; k < KW; ++k) twc[k] = tw[k];
             tac = (int32_t)uni_u32((uint32_t)ta);  // uniform: an SGPR across the barrier
@@ -516,6 +528,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     }
                 }
             }
+        }
+        if constexpr (TL) {  // T words of protein i for the next S5, live only across the barrier
+#pragma unroll
+            for (int k = 0; k < KW; ++k) twc[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
         }
         stamp(5);
         // recycle the protein-(i+2) counter set (last read by S4(i-1))

@@ -46,7 +46,7 @@ if a.v2:
     names = ["T issue + S3", "M/S2/S1 issue", "S5 normalise", "S4 prefetched", "S4 further rounds", "long runs",
              "barrier"]
 else:
-    names = ["T + S4a issue", "S3 tasks", "S2/S1 issue", "T-word carry", "S4b round 1", "S4b rounds 2+/whole",
+    names = ["S4a issue", "S3 tasks", "S2/S1 issue", "-", "S4b round 1", "S4b rounds 2+/whole + T issue",
              "recycle+barrier", "S5 normalise (first)"]
 K = len(names)
 used = c[:, 0, :K].sum(axis=1) > 0
