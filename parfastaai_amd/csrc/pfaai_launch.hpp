@@ -172,6 +172,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "nk1br_v6") { launch_pl<MODE, 5, 1024, 8, 1, true, 6>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "tearly") { launch_pl<MODE, 5, 1024, 8, 1, true, 32>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "g4") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "s3skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "s123skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 192>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

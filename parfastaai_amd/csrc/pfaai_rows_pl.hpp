@@ -264,8 +264,16 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // S1 / S2 return the raw loads: nothing may touch a prefetched value
     // before its consumer, or the compiler waits for it on the spot.
     auto glen = [&](int p) -> uint32_t { return p < P ? uni_u32(goff[p + 1]) - uni_u32(goff[p]) : 0u; };
+    // a wave none of whose entries tid + j*NT is below the list length n has
+    // nothing to do in S1-S3 for that protein (the typical list holds ~290 of
+    // the 1024 entries: 11 of 16 waves are idle); VAR bit 64 skips S3, bit
+    // 128 S1 and S2 as well -- a wave-uniform branch
+    const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
     auto s1 = [&](int p, int32_t (&gt)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
         const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
+        if constexpr ((VAR & 128) != 0) {
+            if (wbase0 >= n) return;
+        }
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
@@ -274,6 +282,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
     auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT]) {  // run-table entries ({0..} past the list)
         const uint32_t n = glen(p);
+        if constexpr ((VAR & 128) != 0) {
+            if (wbase0 >= n) return;
+        }
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
@@ -282,6 +293,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
     auto s3 = [&](int q, const uint4 (&r4)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
+        if constexpr ((VAR & 64) != 0) {
+            if (wbase0 >= glen(q)) return;
+        }
         uint32_t nl[EPT], v = 0;
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
