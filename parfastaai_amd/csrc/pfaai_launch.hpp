@@ -14,7 +14,8 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + (NK == 1 ? (size_t)KW * NT * 2 : 0) +
+    const size_t nbytes = NK != 1 ? 0 : (VAR & 1024) ? (size_t)KW * NT * 2 : (size_t)(KW + 1) / 2 * NT * 4;  // N (u8)
+    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + nbytes +
                        (((size_t)c->prob.n_prot + 1) / 2) * sizeof(uint32_t);  // + T[p][A] (u16)
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
@@ -147,7 +148,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
             const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t) + 5 * 1024 * 2 +
+            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t) + 3 * 1024 * 4 +
                                (((size_t)c->prob.n_prot + 1) / 2) * sizeof(uint32_t);
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
             hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, true, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
@@ -172,8 +173,8 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "nk1br_v6") { launch_pl<MODE, 5, 1024, 8, 1, true, 6>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "tearly") { launch_pl<MODE, 5, 1024, 8, 1, true, 32>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "g4") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "s3skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "s123skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 192>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "noskip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "n16") { launch_pl<MODE, 5, 1024, 8, 1, true, 1024>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

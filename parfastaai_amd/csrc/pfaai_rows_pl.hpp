@@ -231,14 +231,23 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
-    uint16_t* n16 = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1);  // NL: N of columns (2w, 2w+1) as u8 pair
-    uint16_t* taL = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1 + (NL ? W / 2 : 0));  // T[p][A], p < P
+    // NL: N of the thread's columns as u8 in LDS: NPK (default) u32
+    // n32[tid + (k >> 1) * NT] holds word tid + k * NT's two columns, k even
+    // in bytes (0, 2), k odd in bytes (1, 3), so S5 updates it by one packed
+    // min (+ a shift) and a no-return LDS atomic at a constant offset instead
+    // of a read, 7 VALU ops and a write (10.13 -> 9.77 ms at 10k); VAR bit
+    // 1024 keeps the first form, u16 n16[w] = the u8 pair of word w (A/B)
+    constexpr bool NPK = NL && (VAR & 1024) == 0;
+    constexpr int NWORDS = !NL ? 0 : NPK ? (KW + 1) / 2 * NT : W / 2;
+    uint16_t* n16 = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1);
+    uint32_t* n32 = pl_smem + 2 * W + P + 1;
+    uint16_t* taL = reinterpret_cast<uint16_t*>(pl_smem + 2 * W + P + 1 + NWORDS);  // T[p][A], p < P
 
     const int64_t g0 = d.G_off[(int64_t)a * P];
     for (int p = tid; p <= P; p += NT) goff[p] = (uint32_t)(d.G_off[(int64_t)a * P + p] - g0);
     for (int w = tid; w < 2 * W; w += NT) acc[w] = 0u;
     if (NL)
-        for (int w = tid; w < W; w += NT) n16[w] = 0u;
+        for (int w = tid; w < NWORDS; w += NT) n32[w] = 0u;
     if (tid < 3) { ntask[tid] = 0u; nwhole[tid] = 0u; }
     for (int w = tid; w < 3 * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
     const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
@@ -266,12 +275,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     auto glen = [&](int p) -> uint32_t { return p < P ? uni_u32(goff[p + 1]) - uni_u32(goff[p]) : 0u; };
     // a wave none of whose entries tid + j*NT is below the list length n has
     // nothing to do in S1-S3 for that protein (the typical list holds ~290 of
-    // the 1024 entries: 11 of 16 waves are idle); VAR bit 64 skips S3, bit
-    // 128 S1 and S2 as well -- a wave-uniform branch
+    // the 1024 entries: 11 of 16 waves are idle), so it skips them -- a
+    // wave-uniform branch (10.17 -> 9.96 ms at 10k; VAR bit 64 restores the
+    // unconditional form for A/B)
+    constexpr bool kSkip = (VAR & 64) == 0;
     const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
     auto s1 = [&](int p, int32_t (&gt)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
         const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
-        if constexpr ((VAR & 128) != 0) {
+        if constexpr (kSkip) {
             if (wbase0 >= n) return;
         }
 #pragma unroll
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
     auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT]) {  // run-table entries ({0..} past the list)
         const uint32_t n = glen(p);
-        if constexpr ((VAR & 128) != 0) {
+        if constexpr (kSkip) {
             if (wbase0 >= n) return;
         }
 #pragma unroll
@@ -293,7 +304,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
     auto s3 = [&](int q, const uint4 (&r4)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
-        if constexpr ((VAR & 64) != 0) {
+        if constexpr (kSkip) {
             if (wbase0 >= glen(q)) return;
         }
         uint32_t nl[EPT], v = 0;
@@ -372,7 +383,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         } else if constexpr (NK == 2) {
             N[k >> 1] += (min(v & 0xFFFFu, 1u) | (min(v >> 16, 1u) << 16)) << (8 * (k & 1));
         } else {
-            if constexpr ((VAR & 4) != 0)  // first form (A/B)
+            if constexpr (NPK) {
+                const uint32_t x = pk_min1_u16(v);  // (min(c0, 1), min(c1, 1)) at bits 0, 16
+                atomicAdd(&n32[tid + (k >> 1) * NT], (k & 1) ? x << 8 : x);
+            } else if constexpr ((VAR & 4) != 0)  // first form (A/B)
                 n16[w] = (uint16_t)(n16[w] + (uint32_t)((v & 0xFFFFu) != 0u) + ((uint32_t)((v >> 16) != 0u) << 8));
             else
                 n16[w] = (uint16_t)(n16[w] + min(v & 0xFFFFu, 1u) + (min(v >> 16, 1u) << 8));
@@ -391,7 +405,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
             for (int k = 0; k < KW; ++k) {
                 const int32_t w = tid + k * NT;
-                const uint32_t v = acc_p[w];  // (a wave-uniform skip past ncw measured 2 % slower)
+                // (a wave-uniform skip past ncw measured 2 % slower; read and
+                // clear by one ds_wrxchg_rtn_b32: no faster)
+                const uint32_t v = acc_p[w];
                 if (v) {
                     acc_p[w] = 0u;
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
@@ -574,7 +590,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             if (b < wlo || b >= whi || !col_valid<MODE>(d, a, b)) continue;
             const int64_t idx = pair_index<MODE>(d, a, b, compat);
             double s = S[2 * k + h];
-            int32_t n = NK == 1 ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu)
+            int32_t n = NPK ? (int32_t)((n32[tid + (k >> 1) * NT] >> (8 * (k & 1) + 16 * h)) & 0xFFu)
+                        : NK == 1 ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu)
                         : NK == 2 ? (int32_t)((N[(k >> 1) % NN] >> (8 * (k & 1) + 16 * h)) & 0xFFu)
                                   : (int32_t)((N[k % NN] >> (16 * h)) & 0xFFFFu);
             if (n == 0 && compat) {

@@ -65,6 +65,14 @@ __device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi
     return nl;
 }
 
+// (min(lo16, 1), min(hi16, 1)) of a packed u16 pair: one v_pk_min_u16 (the
+// compiler turns the vector-min builtin into two compares and selects)
+__device__ __forceinline__ uint32_t pk_min1_u16(uint32_t v) {
+    uint32_t r;
+    asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "s"(0x00010001u));
+    return r;
+}
+
 // c / d for integers 1 <= c <= 65535, c <= d < 2^17 (T < 2^16 is checked at
 // load), bit-identical to IEEE division: the reciprocal, Newton refinement
 // and final residual correction the compiler expands '/' into (v_rcp_f64,
