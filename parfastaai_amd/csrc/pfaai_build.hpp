@@ -22,7 +22,8 @@
 
 namespace pfaai {
 
-// G-from-F keys: one workgroup per tetramer block (grid-stride over blocks).
+// G-from-F keys: one workgroup per tetramer block (grid-stride over blocks);
+// record (tetramer, F index).
 __global__ __launch_bounds__(256) void k_gkeys_from_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                       const int32_t* __restrict__ Fg, int32_t P,
                                                       uint32_t* __restrict__ keys, uint2* __restrict__ recs) {
@@ -31,18 +32,36 @@ __global__ __launch_bounds__(256) void k_gkeys_from_f(const int64_t* __restrict_
         for (int64_t i = Lp[t] + threadIdx.x; i < e; i += blockDim.x) {
             const int32_t g = Fg[i];
             keys[i] = (uint32_t)g * (uint32_t)P + (uint32_t)Fp[i];
-            recs[i] = make_uint2((uint32_t)t, (uint32_t)g);
+            recs[i] = make_uint2((uint32_t)t, (uint32_t)i);
         }
     }
 }
 
-// sorted (tetramer, genome) records -> G_tet
-__global__ void k_gtet_split(const uint2* __restrict__ recs, int64_t n, int32_t* __restrict__ G_tet) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        G_tet[i] = (int32_t)recs[i].x;
+// sorted (tetramer, F index) records -> G_tet and (if wanted) G_pos, the F
+// index of every G entry
+__global__ void k_gtet_split(const uint2* __restrict__ recs, int64_t n, int32_t* __restrict__ G_tet,
+                             uint32_t* __restrict__ G_pos) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint2 r = recs[i];
+        G_tet[i] = (int32_t)r.x;
+        if (G_pos) G_pos[i] = r.y;
+    }
 }
 
-// F-from-G keys: one wave per (genome, protein) list, lanes over its entries.
+// F from G: sorted keys (tetramer * P + protein) and (genome, G index)
+// records -> the F columns, and G_pos[G index] = F index (if wanted)
+__global__ void k_f_split_pos(const uint32_t* __restrict__ keys, const uint2* __restrict__ recs, int64_t n, int32_t P,
+                              int32_t* __restrict__ fp, int32_t* __restrict__ fg, uint32_t* __restrict__ G_pos) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint2 r = recs[i];
+        fp[i] = (int32_t)(keys[i] % (uint32_t)P);
+        fg[i] = (int32_t)r.x;
+        if (G_pos) G_pos[r.y] = (uint32_t)i;
+    }
+}
+
+// F-from-G keys: one wave per (genome, protein) list, lanes over its entries;
+// record (genome, G index).
 __global__ __launch_bounds__(256) void k_fkeys_from_g(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
                                                       int64_t n_lists, int32_t P, uint32_t* __restrict__ keys,
                                                       uint2* __restrict__ recs, uint32_t* __restrict__ lc) {
@@ -54,7 +73,7 @@ __global__ __launch_bounds__(256) void k_fkeys_from_g(const int64_t* __restrict_
         for (int64_t k = G_off[L] + lane; k < e; k += 64) {
             const uint32_t t = (uint32_t)G_tet[k];
             keys[k] = t * (uint32_t)P + p;
-            recs[k] = make_uint2(p, g);
+            recs[k] = make_uint2(g, (uint32_t)k);
             atomicAdd(&lc[t], 1u);
         }
     }

@@ -60,7 +60,7 @@ struct pfaai_ctx {
     DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
     int64_t max_glen = 0;  // longest (genome, protein) G list
     DevBuf Fp16;
-    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, blk;
+    DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, G_pos, blk;
     bool has_g = false;
     bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
     bool runs_key = false;
@@ -117,6 +117,7 @@ using namespace pfaai;
 // work lists) serves F-only input.  PFAAI_ROWS_KERNEL=pl|pl512|fused|worklist
 // overrides the choice (A/B runs, tools/gpu/ab_rows.py; tests).
 constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
+constexpr int32_t kGposMaxIds = 20480;  // G_pos built for all-vs-all problems up to two row chunks wide
 
 enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3, RK_V2 = 4 };
 

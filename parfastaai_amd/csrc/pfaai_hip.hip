@@ -361,12 +361,13 @@ int build_f_from_g(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
     if ((rc = scan_u32(c, lc, PFAAI_NTETRAMERS, static_cast<unsigned long long*>(c->Lp.p), s))) return rc;
     if (n) {
         auto* recs = static_cast<uint2*>(c->recs.p);
+        const uint32_t* ksorted = nullptr;
         if ((rc = radix_sort_recs(c, static_cast<const uint32_t*>(c->key_c.p), n, bits_for((int64_t)PFAAI_NTETRAMERS * P),
-                                  static_cast<const uint2*>(c->rec_c.p), recs, s, nullptr)))
+                                  static_cast<const uint2*>(c->rec_c.p), recs, s, &ksorted)))
             return rc;
         const int g2 = (int)std::min<int64_t>(ceil_div(n, 256), 1 << 16);
-        hipLaunchKernelGGL(k_f_split, dim3(g2), dim3(256), 0, s, recs, n, static_cast<int32_t*>(c->Fp.p),
-                           static_cast<int32_t*>(c->Fg.p));
+        hipLaunchKernelGGL(k_f_split_pos, dim3(g2), dim3(256), 0, s, ksorted, recs, n, P, static_cast<int32_t*>(c->Fp.p),
+                           static_cast<int32_t*>(c->Fg.p), static_cast<uint32_t*>(c->G_pos.p));
         HIPCHK(c, hipGetLastError());
     }
     return PFAAI_RC_OK;
@@ -397,7 +398,8 @@ int build_g_from_f(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
                               static_cast<const uint2*>(c->rec_c.p), recs, s, &ksorted)))
         return rc;
     const int g2 = (int)std::min<int64_t>(ceil_div(n, 256), 1 << 16);
-    hipLaunchKernelGGL(k_gtet_split, dim3(g2), dim3(256), 0, s, recs, n, static_cast<int32_t*>(c->G_tet.p));
+    hipLaunchKernelGGL(k_gtet_split, dim3(g2), dim3(256), 0, s, recs, n, static_cast<int32_t*>(c->G_tet.p),
+                       static_cast<uint32_t*>(c->G_pos.p));
     hipLaunchKernelGGL(k_rowptr, dim3(ceil_div(n, 256)), dim3(256), 0, s, ksorted, n, n_lists, goff);
     HIPCHK(c, hipGetLastError());
     return PFAAI_RC_OK;
@@ -645,7 +647,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     }
     const auto t2 = clk::now();  // uploads done (hipMemcpy is synchronous)
     ms_upload = ms(t1, t2);
+    // G_pos, the F index of every G entry, falls out of either transpose: the
+    // all-vs-all row kernel starts each run walk just past the row genome
+    // (k_rows_pl WK 3); not built for QSUB / QT or rows wider than two chunks
+    bool pos_ok = false;
+    if (p.mode == PFAAI_MODE_ALL && ni <= kGposMaxIds && n_f > 0) {
+        if ((rc = ensure(c, c->G_pos, n_f * sizeof(uint32_t)))) return rc;
+    } else {
+        release(c->G_pos);
+    }
     if (!in_f && (rc = build_f_from_g(c, ng, n_f, s))) return rc;
+    pos_ok = !in_f;
     bool has_g = in_g;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
@@ -673,6 +685,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         release(user_tet);
         if (rc) return rc;
         if (ne) return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
+        pos_ok = true;
     } else if (in_g && in_f && n_f) {  // both given, G larger (QT: both DBs' lists): G must hold F (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
         int* err = reinterpret_cast<int*>(sc + SC_ERR);
@@ -697,12 +710,14 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         HIPCHK(c, hipStreamSynchronize(s));
         for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, goff[k + 1] - goff[k]);
         has_g = true;
+        pos_ok = true;
     }
     c->has_g = has_g;
     if (!has_g) {
         release(c->G_off);
         release(c->G_tet);
     }
+    if (!has_g || !pos_ok) release(c->G_pos);
     if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
     HIPCHK(c, hipMemsetAsync(c->Fp16.p, 0, (n_f + 16) * sizeof(uint16_t), s));
     if (n_f)
@@ -732,6 +747,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
     d.G_off = has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
     d.G_tet = has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
+    d.G_pos = c->G_pos.p ? static_cast<const uint32_t*>(c->G_pos.p) : nullptr;
     d.blk = has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
     d.Fp16 = static_cast<const uint16_t*>(c->Fp16.p);
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
@@ -788,7 +804,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw})
         release(*b);

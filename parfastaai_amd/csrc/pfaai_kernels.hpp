@@ -60,6 +60,7 @@ struct Dev {
     const int32_t* tcol_col;    // [n_ids] T column used when the genome is genomeB
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
+    const uint32_t* G_pos;      // [|G|] F index of each G entry (all-vs-all; nullptr if not built)
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
     const uint16_t* Fp16;       // [|F|] protein of each F entry, u16 (k_blk)
     const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)

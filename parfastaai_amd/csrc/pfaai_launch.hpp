@@ -24,6 +24,9 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     // id, so all-vs-all rows test only b > a and -q / full rows test nothing
     constexpr int kWk1 = MODE == 0 ? 1 : MODE == 2 ? 0 : 2;
     const int wk = nchunks == 1 && !DIAG_ENV("PFAAI_PL_WK0") ? kWk1 : 0;
+    // all-vs-all rows in one chunk with G_pos loaded: each run walk starts just
+    // past the row genome (k_rows_pl WK 3, pl_issue_m2<A8>)
+    const bool gp = MODE == 0 && wk == 1 && c->dev.G_pos && !DIAG_ENV("PFAAI_PL_NOGPOS");
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #define PLK(BF, WKV)                                                                                                 \
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, WKV>), dim3(r1 - r0, gy), dim3(NT), lds, \
@@ -31,6 +34,12 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         if (wk == 0 || abs_chunk >= 0) {
             if (bigf) PLK(true, 0); else PLK(false, 0);
         } else if constexpr (kWk1 != 0) {
+            if constexpr (MODE == 0) {
+                if (gp) {
+                    if (bigf) PLK(true, 3); else PLK(false, 3);
+                    return;
+                }
+            }
             if (bigf) PLK(true, kWk1); else PLK(false, kWk1);
         }
 #undef PLK

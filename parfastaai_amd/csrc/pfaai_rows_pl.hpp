@@ -130,7 +130,8 @@ __device__ __forceinline__ uint32_t pl_issue_m(rsrc_t fg, const int32_t* __restr
 
 // WK: the window test a member needs -- 0: wlo <= b < whi; 1: wlo <= b (the
 // window reaches the last id, e.g. an all-vs-all row in one chunk); 2: none
-// (the window is every id, e.g. a full row).
+// (the window is every id, e.g. a full row); 3: none (the members after A in
+// a run, all-vs-all with G_pos, see pl_issue_m2).
 template <int MODE, int WK>
 __device__ __forceinline__ void pl_add_m(const Dev& d, int32_t a, int32_t b, bool valid, uint32_t* accb, int32_t wlo,
                                          uint32_t wspan) {
@@ -154,12 +155,20 @@ __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, 
 // Two-lane groups (the k_rows_pl default): a lane takes half a line task, 8
 // members by two 16-B loads, so a protein's tasks fill half as many wave
 // rounds and the per-task issue work is shared by 8 members instead of 4.
-template <int TC = kPlTaskCap, bool BIGF = false>
+// A8 (WK 3, all-vs-all rows in one chunk, G_pos loaded): a run's members
+// after the row genome A are exactly its partners b > A (runs are sorted by
+// genome), so the tasks are 16-member spans of [G_pos + 1, run end) from an
+// 8-aligned start, and the members need no window test -- instead of the
+// run's 16-aligned lines pruned only at line granularity by the splitters
+// (SYN 10k: 50 % of the loaded member slots were events).  8-member tasks,
+// one per lane, overflow the 2048-entry task list for low rows (up to 4 200
+// per protein at 10k: 13.3 ms vs 9.8).
+template <int TC = kPlTaskCap, bool BIGF = false, bool A8 = false>
 __device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
                                                 const uint2* rt, int k, int nt, uint32_t gl8, uint4& b, uint4& bh) {
     const uint32_t t = tk[min(k, TC - 1)];
     const uint2 rr = rt[t & 1023u];
-    const uint32_t m0 = (rr.x & ~(uint32_t)(kGroup - 1)) + ((t >> 6) & ~15u) + gl8;
+    const uint32_t m0 = (rr.x & ~(uint32_t)(A8 ? 7 : kGroup - 1)) + ((t >> 6) & ~15u) + gl8;
     const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 8);
     const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 8);
     uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
@@ -280,7 +289,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // unconditional form for A/B)
     constexpr bool kSkip = (VAR & 64) == 0;
     const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
-    auto s1 = [&](int p, int32_t (&gt)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
+    // WK 3: S1 also loads each entry's G_pos, S2 carries it on (gq -> gq2)
+    // and loads only the run's end; S3 cuts [G_pos + 1, end) into 16-member
+    // tasks from an 8-aligned start (pl_issue_m2<A8>)
+    constexpr bool GP = WK == 3;
+    const rsrc_t r_gp = mk_rsrc(GP ? d.G_pos + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
+    auto s1 = [&](int p, int32_t (&gt)[EPT], uint32_t (&gq)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
         const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
         if constexpr (kSkip) {
             if (wbase0 >= n) return;
@@ -289,9 +303,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
             gt[j] = (int32_t)bld_u32(r_g, e < n ? e * 4u : kOOB, o * 4u);
+            if constexpr (GP) gq[j] = bld_u32(r_gp, e < n ? e * 4u : kOOB, o * 4u);
         }
     };
-    auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT]) {  // run-table entries ({0..} past the list)
+    auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT], const uint32_t (&gq)[EPT], uint32_t (&gq2)[EPT]) {
+        // run-table entries ({0..} past the list)
         const uint32_t n = glen(p);
         if constexpr (kSkip) {
             if (wbase0 >= n) return;
@@ -299,10 +315,17 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
-            r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB, (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+            if constexpr (GP) {
+                gq2[j] = gq[j];
+                r4[j].y = bld_u32(r_blk, e < n ? (uint32_t)gt[j] * 16u + 4u : kOOB,
+                                  (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+            } else {
+                r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB,
+                                 (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+            }
         }
     };
-    auto s3 = [&](int q, const uint4 (&r4)[EPT]) {  // line tasks of protein q
+    auto s3 = [&](int q, const uint4 (&r4)[EPT], const uint32_t (&gq2)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
         if constexpr (kSkip) {
             if (wbase0 >= glen(q)) return;
@@ -312,7 +335,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int j = 0; j < EPT; ++j) {
             const int e = tid + j * NT;
             uint2 r;
-            nl[j] = run_lines(r4[j], wlo, whi, r, min_len);
+            if constexpr (GP) {
+                r = make_uint2(gq2[j] + 1u, r4[j].y);  // OOB entries: (1, 0), empty
+                nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
+            } else {
+                nl[j] = run_lines(r4[j], wlo, whi, r, min_len);
+            }
             rt[st][e] = r;
             if (nl[j] > (uint32_t)kPlMaxLines) {
                 atomicOr(&wmask[cs][e >> 5], 1u << (e & 31));
@@ -352,12 +380,15 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // prologue: tasks of protein 0; run-table entries of protein 1; G lists of protein 2
     int32_t gt[EPT];
     uint4 r4[EPT];
-    s1(0, gt);
-    s2(0, gt, r4);
-    s1(1, gt);
-    s3(0, r4);
-    s2(1, gt, r4);
-    s1(2, gt);
+    uint32_t gq[EPT], gq2[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) { r4[j] = make_uint4(0u, 0u, 0u, 0u); gq[j] = gq2[j] = 0u; }
+    s1(0, gt, gq);
+    s2(0, gt, r4, gq, gq2);
+    s1(1, gt, gq);
+    s3(0, r4, gq2);
+    s2(1, gt, r4, gq, gq2);
+    s1(2, gt, gq);
     __syncthreads();
 
     unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -449,8 +480,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // (10.60 -> 10.47 ms, VALU instructions -5.8 % at 10k); VAR bit 8 keeps the
     // four-lane groups with two tasks in flight, VAR bit 2 the first form
     // (pl_issue / pl_scatter4), for A/B
-    constexpr bool kLegacyM = (VAR & 2) != 0;
-    constexpr bool G2 = (VAR & 8) == 0 && !kLegacyM;
+    constexpr bool kLegacyM = (VAR & 2) != 0 && !GP;
+    constexpr bool G2 = ((VAR & 8) == 0 && !kLegacyM) || GP;
     constexpr int NGX = G2 ? NT / 2 : NG;
     const int grpx = G2 ? tid >> 1 : grp;
     const uint32_t gl8 = 8u * (uint32_t)(tid & 1);
@@ -467,7 +498,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         else pl_scatter4_m<MODE, WK>(d, a, bb, m, acc_x - (cc0 >> 1), wlo, wspan);
     };
     auto issue2 = [&](int k, int ntk, uint4& bb, uint4& bbh) -> uint32_t {
-        return pl_issue_m2<TC, BIGF>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
+        return pl_issue_m2<TC, BIGF, GP>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
     };
     auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
         pl_scatter4_m<MODE, WK>(d, a, bb, m & 15u, acc_x - (cc0 >> 1), wlo, wspan);
@@ -504,10 +535,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t okm = G2 ? issue2(grpx, nt, b, bh) : issue(grp, nt, b);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
-        if (i + 1 < P) s3(i + 1, r4);
+        if (i + 1 < P) s3(i + 1, r4, gq2);
         stamp(1);
-        s2(i + 2, gt, r4);
-        s1(i + 3, gt);
+        s2(i + 2, gt, r4, gq, gq2);
+        s1(i + 3, gt, gq);
         stamp(2);
         if (prio) __builtin_amdgcn_s_setprio(0);
         // S5: normalise protein i-1

@@ -13,7 +13,7 @@
 #define VARP 0
 #endif
 #ifndef WKP
-#define WKP 1
+#define WKP 3
 #endif
 #ifndef BRP
 #define BRP true
