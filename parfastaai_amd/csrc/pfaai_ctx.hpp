@@ -64,6 +64,7 @@ struct pfaai_ctx {
     bool has_g = false;
     bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
     bool runs_key = false;
+    bool runs_ends = false;  // the run table holds u32 run ends only (k_blk_end, k_rows_pl WK 3)
     bool wl_ready = false;  // work-list buffers allocated (ensure_worklists)
     pfaai::Dev dev{};
 
@@ -187,6 +188,16 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
     if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->cols_run, 5);
     const char* km = getenv("PFAAI_PL_KWMAX");
     return 2 * 1024 * (int64_t)pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
+}
+
+// k_rows_pl WK 3 -- all-vs-all rows in one chunk with G_pos loaded -- reads
+// only the END of each G entry's run, so the step builds the u32 end table
+// (k_blk_end) instead of k_blk's 16-B entries.  One predicate for the run
+// table build (run_mode) and the kernel choice (launch_pl).
+inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
+    return mode == 0 && c->rows_kernel == RK_PL && c->dev.G_pos && !c->windows &&
+           ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
+           !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");
 }
 
 // Row kernels for output rows [rb, re) (pfaai_launch.hpp; instantiated per

@@ -172,7 +172,18 @@ int launch_first_key(pfaai_ctx* c, hipStream_t s) {
 // Fused genome-major path: only the run table (+ the first E triple for the
 // ref-compat zero-overlap quirk); k_rows walks the G lists itself.
 template <int MODE>
-int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event) {
+int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
+    if (ends) {  // k_rows_pl WK 3 reads run ends only (pl_uses_ends)
+        const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkEndTileMax, kBlkLdsBytes / (4 * c->prob.n_prot)));
+        hipLaunchKernelGGL((k_blk_end<1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024),
+                           (size_t)c->prob.n_prot * tile * sizeof(uint32_t), s, c->dev, tile);
+        if (first_event) {
+            const int rc = launch_first_key(c, s);
+            if (rc) return rc;
+        }
+        HIPCHK(c, hipGetLastError());
+        return PFAAI_RC_OK;
+    }
     const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
     const int dbg = DIAG_ENV("PFAAI_BLK_ABLATE") ? atoi(DIAG_ENV("PFAAI_BLK_ABLATE")) : 0;
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
@@ -305,7 +316,9 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     // PFAAI_FLAG_KEEP_RUNS: the run table depends only on the loaded F, so a
     // run over further rows of the same problem may reuse it (stream-ordered
     // after the run that built it)
-    const bool keep = !wl && (flags & PFAAI_FLAG_KEEP_RUNS) && c->runs_valid && (c->runs_key || !compat);
+    const bool ends = !wl && pl_uses_ends(c, MODE);  // which table launch_rows will read
+    const bool keep = !wl && (flags & PFAAI_FLAG_KEEP_RUNS) && c->runs_valid && (c->runs_key || !compat) &&
+                      c->runs_ends == ends;
     int rc = PFAAI_RC_OK;
     if constexpr (MODE == kModeFull) {
         if (wl) return fail(c, PFAAI_RC_INVALID, "full rows need the genome-major path");
@@ -313,9 +326,10 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         rc = build_records<MODE>(c, rb, re, s, compat);
     }
     if (!wl && !keep) {
-        rc = build_runs_g<MODE>(c, s, compat);
+        rc = build_runs_g<MODE>(c, s, compat, ends);
         c->runs_valid = rc == PFAAI_RC_OK;
         c->runs_key = compat;
+        c->runs_ends = ends;
     }
     if (rc) return rc;
     HIPCHK(c, hipEventRecord(c->ev1, s));

@@ -420,6 +420,63 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
     }
 }
 
+// k_blk_end: the run-END table alone, ends[p * 160000 + t] = one past the
+// last F entry of run (t, p), u32, p-major.  It is all k_rows_pl WK 3 reads
+// (all-vs-all rows in one chunk with G_pos loaded: a run walk starts at the
+// row genome's own F position + 1, so neither the run start nor the line
+// splitters are needed): k_blk's phase (1) for tails only, staged as u32 in
+// LDS for up to 64 tetramers per workgroup.  Reads 2 B per F entry (Fp16),
+// writes 4 B per (protein, tetramer) slot -- a quarter of k_blk's table, and
+// no pass over Fg.
+constexpr int kBlkEndTileMax = 64;
+
+template <int NTH>
+__global__ __launch_bounds__(NTH) void k_blk_end(Dev d, int tile) {
+    extern __shared__ uint32_t ende[];  // [tile][n_prot], tetramer-major
+    __shared__ int64_t lp[kBlkEndTileMax + 1];
+    const int tid = threadIdx.x, lane = tid & 63, P = d.n_prot;
+    const int t0 = blockIdx.x * tile;
+    const int nt = min(tile, kNTetramers - t0);
+    for (int k = tid; k < tile * P; k += NTH) ende[k] = 0u;
+    if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
+    __syncthreads();
+    const int64_t S = lp[0], E = lp[nt];
+    for (int64_t c0 = (S & ~(int64_t)7) + (int64_t)tid * 8; c0 - (int64_t)lane * 8 < E; c0 += (int64_t)NTH * 8) {
+        const bool in = c0 < E;  // wave-uniform trip count (DPP needs the whole wave)
+        const uint4 v = in ? *reinterpret_cast<const uint4*>(d.Fp16 + c0) : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.x & 0xFFFFu), 0x130, 0xf, 0xf, false);  // wave_shl:1
+        if (lane == 63) next = c0 + 8 < E ? d.Fp16[c0 + 8] : 0xFFFFu;
+        if (!in) continue;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int64_t i0 = max(c0, S);
+        int lo = 0, hi = nt - 1;  // tetramer of entry i0: last tl with lp[tl] <= i0
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lp[mid] <= i0) lo = mid; else hi = mid - 1;
+        }
+        int tl = lo;
+        int64_t nb = lp[tl + 1];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t i = c0 + j;
+            const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
+            if (i < S || i >= E) continue;
+            if (i >= nb) {  // crossed into a later tetramer block
+                while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
+                nb = lp[tl + 1];
+            }
+            if (i + 1 == nb || qn != q) ende[tl * P + q] = (uint32_t)(i + 1);
+        }
+    }
+    __syncthreads();
+    uint32_t* ends = reinterpret_cast<uint32_t*>(d.blk);
+    for (int k = tid; k < tile * P; k += NTH) {
+        const int tl = k % tile, q = k / tile;  // one protein's consecutive tetramers per run of lanes
+        if (tl < nt) ends[(int64_t)q * kNTetramers + t0 + tl] = ende[tl * P + q];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K-W2: stable LSD radix sort of the (key, entry) pairs, 8-bit digits.
 // Tiles of 4096 keys (256 threads x 16, striped so loads coalesce).  Per

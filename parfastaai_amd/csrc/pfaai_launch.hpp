@@ -26,7 +26,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     const int wk = nchunks == 1 && !DIAG_ENV("PFAAI_PL_WK0") ? kWk1 : 0;
     // all-vs-all rows in one chunk with G_pos loaded: each run walk starts just
     // past the row genome (k_rows_pl WK 3, pl_issue_m2<A8>)
-    const bool gp = MODE == 0 && wk == 1 && c->dev.G_pos && !DIAG_ENV("PFAAI_PL_NOGPOS");
+    const bool gp = MODE == 0 && wk == 1 && pl_uses_ends(c, MODE);
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #define PLK(BF, WKV)                                                                                                 \
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, WKV>), dim3(r1 - r0, gy), dim3(NT), lds, \

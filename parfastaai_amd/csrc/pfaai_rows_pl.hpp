@@ -276,7 +276,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // that crosses num_records reads all zeros, not just its tail
     const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)(d.n_f + 16) * 4u);
     const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
-    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked)
+    // the run table: 16-B entries (k_blk), or u32 run ends under WK 3 (k_blk_end)
+    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * (WK == 3 ? 4u : 16u));  // < 4 GiB: P <= 1600 (host-checked)
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);
     const rsrc_t r_t = mk_rsrc(d.T, (uint64_t)P * d.t_cols * 4u);
     // S1 / S2 return the raw loads: nothing may touch a prefetched value
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr bool kSkip = (VAR & 64) == 0;
     const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
     // WK 3: S1 also loads each entry's G_pos, S2 carries it on (gq -> gq2)
-    // and loads only the run's end; S3 cuts [G_pos + 1, end) into 16-member
+    // and loads only the run's end (from k_blk_end's u32 table); S3 cuts [G_pos + 1, end) into 16-member
     // tasks from an 8-aligned start (pl_issue_m2<A8>)
     constexpr bool GP = WK == 3;
     const rsrc_t r_gp = mk_rsrc(GP ? d.G_pos + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
@@ -317,8 +318,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             const uint32_t e = (uint32_t)(tid + j * NT);
             if constexpr (GP) {
                 gq2[j] = gq[j];
-                r4[j].y = bld_u32(r_blk, e < n ? (uint32_t)gt[j] * 16u + 4u : kOOB,
-                                  (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+                r4[j].y = bld_u32(r_blk, e < n ? (uint32_t)gt[j] * 4u : kOOB,
+                                  (uint32_t)min(p, P - 1) * (kNTetramers * 4u));
             } else {
                 r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB,
                                  (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
