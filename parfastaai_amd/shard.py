@@ -11,13 +11,14 @@ from __future__ import annotations
 
 
 # Device time of an all-vs-all row ~ (fixed + width): every row walks its
-# genome's full G lists (P protein iterations, each a latency chain) whatever
-# its width, then pays per column.  Measured on MI355X at 10k x 100 SCPs
-# (tools/gpu/ab_rows.py --rows): 2000 rows of mean width 9000 take 3.65 ms,
-# 2000 rows of mean width 1000 take 1.90 ms, i.e. fixed ~ 0.77 x n columns.
-# Balancing by pairs alone would give the last rank (narrow rows) ~3x the
-# time of the first.
-FIXED_COST_FRACTION = 0.75
+# genome's full G lists (P protein iterations, each a latency chain with one
+# workgroup barrier) whatever its width, then pays per column.  Fitted on
+# MI355X at 10k x 100 SCPs from the 8-way shard times of candidate splits
+# (tools/gpu/shard_times.py, SHARD_FRACS; profiles/r02g_shard_times_10k_x8.txt):
+# fixed = 0.75 n -> slowest shard 1.45 ms, 1.0 n -> 1.36, 1.25 n -> 1.32,
+# 1.5 n -> 1.33, 2.0 n -> 1.43 (mean 1.26).  Balancing by pairs alone gives
+# the last rank (narrow rows) 2.7 ms.
+FIXED_COST_FRACTION = 1.25
 
 
 def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: float | None = None):

@@ -21,7 +21,9 @@ eng.load(**ds.problem())
 rows, pairs = eng.shape()
 d = eng.alloc(pairs * 8)
 eng.run(0, rows, 0, d)
-for label, kw in (("cost model", {}), ("pair balance", {"fixed_cols": 0})):
+fracs = [float(x) for x in os.environ.get("SHARD_FRACS", "").split(",") if x]
+for label, kw in [("cost model", {}), ("pair balance", {"fixed_cols": 0})] + \
+        [(f"fixed {f:.2f}n", {"fixed_cols": f * n}) for f in fracs]:
     blocks = split_rows(rows, world, **kw)
     ms = []
     for rb, re_ in blocks:
@@ -52,4 +54,26 @@ for nch in (1, 2, 4):
             t.append(b + r)
         ms.append(float(np.median(t)))
     print(f"chunks {nch}: k_blk + k_rows ms per shard {[round(x, 3) for x in ms]}  max {max(ms):.3f}")
+
+# row cost profile: k_rows time of n/20-row blocks across the triangle, fitted
+# as t = alpha * rows + beta * pairs -> the cost model's fixed part in column
+# units (FIXED_COST_FRACTION * n = alpha / beta)
+nb = 20
+prof = []
+for i in range(nb):
+    rb, re_ = rows * i // nb, rows * (i + 1) // nb
+    t = []
+    for _ in range(3):
+        eng.timing(reset=True)
+        eng.run(rb, re_, _capi.FLAG_KEEP_RUNS, d)
+        _, b, r = eng.timing(reset=True)
+        t.append(r)
+    npairs = sum(n - 1 - a for a in range(rb, re_))
+    prof.append((re_ - rb, npairs, float(np.median(t))))
+A = np.array([[r, p] for r, p, _ in prof], dtype=float)
+y = np.array([t for _, _, t in prof])
+(alpha, beta), *_ = np.linalg.lstsq(A, y, rcond=None)
+print("row profile (rows, pairs, ms):", [(r, p, round(t, 3)) for r, p, t in prof])
+print(f"fit: {alpha * 1e3:.3f} us per row + {beta * 1e6:.3f} ns per pair -> fixed = {alpha / beta:.0f} columns "
+      f"= {alpha / beta / n:.3f} x n; residuals {[round(v, 3) for v in (A @ [alpha, beta] - y)]}")
 eng.free(d)
