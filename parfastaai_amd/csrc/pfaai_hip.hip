@@ -174,9 +174,18 @@ int launch_first_key(pfaai_ctx* c, hipStream_t s) {
 template <int MODE>
 int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
     if (ends) {  // k_rows_pl WK 3 reads run ends only (pl_uses_ends)
-        const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkEndTileMax, kBlkLdsBytes / (4 * c->prob.n_prot)));
-        hipLaunchKernelGGL((k_blk_end<1024>), dim3(ceil_div(kNTetramers, tile)), dim3(1024),
-                           (size_t)c->prob.n_prot * tile * sizeof(uint32_t), s, c->dev, tile);
+        const char* et = getenv("PFAAI_BLK_END_TILE");  // tetramers per workgroup (A/B)
+        const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(et ? std::min(atoi(et), kBlkEndTileMax) : kBlkEndTileMax,
+                                                                     kBlkLdsBytes / (4 * c->prob.n_prot)));
+        const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint32_t);
+        const char* eu = getenv("PFAAI_BLK_END_U");  // loads in flight per lane (A/B)
+        const int u = eu ? atoi(eu) : 1;
+        if (u >= 4)
+            hipLaunchKernelGGL((k_blk_end<1024, 4>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile);
+        else if (u == 2)
+            hipLaunchKernelGGL((k_blk_end<1024, 2>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile);
+        else
+            hipLaunchKernelGGL((k_blk_end<1024, 1>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile);
         if (first_event) {
             const int rc = launch_first_key(c, s);
             if (rc) return rc;

@@ -430,8 +430,9 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
 // no pass over Fg.
 constexpr int kBlkEndTileMax = 64;
 
-template <int NTH>
-__global__ __launch_bounds__(NTH) void k_blk_end(Dev d, int tile) {
+template <int NTH, int U = 1>
+__global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
+    // (two 1024-thread workgroups per CU: <= 64 VGPRs)
     extern __shared__ uint32_t ende[];  // [tile][n_prot], tetramer-major
     __shared__ int64_t lp[kBlkEndTileMax + 1];
     const int tid = threadIdx.x, lane = tid & 63, P = d.n_prot;
@@ -441,32 +442,42 @@ __global__ __launch_bounds__(NTH) void k_blk_end(Dev d, int tile) {
     if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
     __syncthreads();
     const int64_t S = lp[0], E = lp[nt];
-    for (int64_t c0 = (S & ~(int64_t)7) + (int64_t)tid * 8; c0 - (int64_t)lane * 8 < E; c0 += (int64_t)NTH * 8) {
-        const bool in = c0 < E;  // wave-uniform trip count (DPP needs the whole wave)
-        const uint4 v = in ? *reinterpret_cast<const uint4*>(d.Fp16 + c0) : make_uint4(0u, 0u, 0u, 0u);
-        uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v.x & 0xFFFFu), 0x130, 0xf, 0xf, false);  // wave_shl:1
-        if (lane == 63) next = c0 + 8 < E ? d.Fp16[c0 + 8] : 0xFFFFu;
-        if (!in) continue;
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        const int64_t i0 = max(c0, S);
-        int lo = 0, hi = nt - 1;  // tetramer of entry i0: last tl with lp[tl] <= i0
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (lp[mid] <= i0) lo = mid; else hi = mid - 1;
-        }
-        int tl = lo;
-        int64_t nb = lp[tl + 1];
+    // U: 16-B loads per lane in flight before the first is used
+    for (int64_t cb = (S & ~(int64_t)7) + (int64_t)tid * 8; cb - (int64_t)lane * 8 < E; cb += (int64_t)U * NTH * 8) {
+        uint4 v[U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t i = c0 + j;
-            const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-            const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
-            if (i < S || i >= E) continue;
-            if (i >= nb) {  // crossed into a later tetramer block
-                while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
-                nb = lp[tl + 1];
+        for (int u = 0; u < U; ++u) {
+            const int64_t c0 = cb + (int64_t)u * NTH * 8;
+            v[u] = c0 < E ? *reinterpret_cast<const uint4*>(d.Fp16 + c0) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t c0 = cb + (int64_t)u * NTH * 8;
+            // wave-uniform up to the DPP (it needs the whole wave)
+            uint32_t next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v[u].x & 0xFFFFu), 0x130, 0xf, 0xf, false);  // wave_shl:1
+            if (lane == 63) next = c0 + 8 < E ? d.Fp16[c0 + 8] : 0xFFFFu;
+            if (c0 >= E) continue;
+            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const int64_t i0 = max(c0, S);
+            int lo = 0, hi = nt - 1;  // tetramer of entry i0: last tl with lp[tl] <= i0
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (lp[mid] <= i0) lo = mid; else hi = mid - 1;
             }
-            if (i + 1 == nb || qn != q) ende[tl * P + q] = (uint32_t)(i + 1);
+            int tl = lo;
+            int64_t nb = lp[tl + 1];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t i = c0 + j;
+                const uint32_t q = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                const uint32_t qn = j == 7 ? next : (w[(j + 1) >> 1] >> (16 * ((j + 1) & 1))) & 0xFFFFu;
+                if (i < S || i >= E) continue;
+                if (i >= nb) {  // crossed into a later tetramer block
+                    while (tl + 1 < nt && lp[tl + 1] <= i) ++tl;
+                    nb = lp[tl + 1];
+                }
+                if (i + 1 == nb || qn != q) ende[tl * P + q] = (uint32_t)(i + 1);
+            }
         }
     }
     __syncthreads();

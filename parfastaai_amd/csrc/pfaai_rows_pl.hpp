@@ -140,7 +140,14 @@ __device__ __forceinline__ void pl_add_m(const Dev& d, int32_t a, int32_t b, boo
     if constexpr (WK == 1) ok = ok && b >= wlo;
     if (MODE == 1) ok = ok && b != a && (!d.is_q[b] || b > a);  // isValidPair, ds_impl.hpp:270-273
     if (MODE == kModeFull) ok = ok && b != a;
-    if (ok) atomicAdd(&accb[(uint32_t)b >> 1], 1u << (((uint32_t)b & 1u) << 4));
+    if (ok) {
+        // counter word b >> 1: a v_lshrrev the compiler cannot fold back into
+        // (b << 1) & ~3, so the address is one v_lshl_add (4 VALU per member
+        // instead of 5)
+        uint32_t wi;
+        asm("v_lshrrev_b32 %0, 1, %1" : "=v"(wi) : "v"(b));
+        atomicAdd(&accb[wi], 1u << (((uint32_t)b & 1u) << 4));
+    }
 }
 
 template <int MODE, int WK>
