@@ -102,6 +102,35 @@ def test_keep_runs_matches_single_run(engine):
     assert n_runs >= 3
 
 
+def test_keep_runs_across_table_kinds(engine):
+    """All-vs-all rows read the u32 run-end table (k_blk_end), full rows the
+    16-B run table (k_blk): PFAAI_FLAG_KEEP_RUNS must rebuild whenever the
+    next run needs the other kind, in either order."""
+    import torch
+
+    n = 260
+    pb = _all_problem(n, 30, clade_size=9)
+    engine.load(**pb)
+    aji, _, _ = engine.compute(0)
+    dense = np.zeros((n, n))
+    iu = np.triu_indices(n, 1)
+    dense[iu] = aji
+    dense = dense + dense.T
+    _, npairs = engine.shape()
+    tri = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    full = torch.zeros((n * n,), dtype=torch.float64, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    K, FR = _capi.FLAG_KEEP_RUNS, _capi.FLAG_FULL_ROWS
+    engine.run(0, 100, 0, tri.data_ptr(), stream=st)            # builds the end table
+    engine.run(0, 130, K | FR, full.data_ptr(), stream=st)      # needs the 16-B table
+    engine.run(100, 200, K, tri.data_ptr(), stream=st)          # back to ends
+    engine.run(130, n, K | FR, full.data_ptr(), stream=st)      # and 16-B again
+    engine.run(200, n, K, tri.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    assert np.array_equal(tri.cpu().numpy(), aji)
+    assert np.array_equal(full.cpu().numpy().reshape(n, n), dense)
+
+
 @pytest.mark.timeout(600)
 def test_f_beyond_2_30_entries(engine):
     """|F| > 2^30: member ids past byte offset 2^32 of F (SYN N = 38 000,
