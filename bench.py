@@ -11,9 +11,12 @@ loads it into HBM once (pfaai_load), and owns a contiguous block of output
 rows balanced by a measured row-cost model (parfastaai_amd/shard.py).  One
 step = the hot path over the resident inputs: the run-table build k_blk (the
 reference's E construction, without E) + the scatter/Jaccard/AJI row kernel
-k_rows_pl over the rank's rows; for N > 1 the rows run in --chunks pipeline
-chunks (the run table built once per step) and each chunk's fp64 AJI is
-gathered to rank 0 over RCCL asynchronously while the next chunk computes.
+k_rows_pl over the rank's rows; for N > 1 the rank's fp64 AJI block is
+gathered to rank 0 over RCCL asynchronously, double-buffered so that step
+i + 1 computes while step i's gather is in flight (every step computes and
+gathers its whole block; the timed region ends after the last gather), and
+--chunks > 1 also cuts a step's rows into pipeline chunks, each gathered as
+soon as it is computed (the run table built once per step).
 Total work is fixed as N grows: scaling "strong".  value = genome pairs of
 the whole matrix / max step time over ranks.
 
@@ -160,10 +163,13 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=320)
-    ap.add_argument("--chunks", type=int, default=None,
-                    help="pipeline chunks per rank (gather of chunk j overlaps chunk j+1); "
-                         "default 1 at N = 1, 2 at N > 1 (tools/gpu/shard_times.py: 4 chunks add "
-                         "0.95 ms of launch tails per 10k/8 shard, 2 chunks 0.25 ms)")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="pipeline chunks per rank and step (gather of chunk j overlaps chunk j+1); "
+                         "default 1: the gather overlaps the next step instead (tools/gpu/shard_times.py: "
+                         "2 chunks add 0.38 ms of launch tails per 10k/8 shard, 4 chunks 0.87 ms)")
+    ap.add_argument("--slots", type=int, default=None,
+                    help="AJI buffer sets per rank: 2 (default at N > 1) lets step i + 1 compute while "
+                         "step i's gather is in flight; 1 waits for each step's gather")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     args = ap.parse_args()
@@ -199,23 +205,31 @@ def main():
     spans = [eng.row_span(rb, re) for rb, re in blocks]
     rb, re = blocks[rank]
     first, count = spans[rank]
-    # N > 1: the rank's rows in pipeline chunks; chunk j's AJI is gathered to
-    # rank 0 (RCCL, async) while chunk j+1 computes; the run table is built
-    # by chunk 0 only (PFAAI_FLAG_KEEP_RUNS)
-    nch = max(1, args.chunks) if args.chunks else (1 if world == 1 else 2)
+    # N > 1: the rank's AJI block is gathered to rank 0 (RCCL, async); with
+    # two buffer sets the gather of step i overlaps the compute of step i + 1.
+    # --chunks > 1: the rows in pipeline chunks, chunk j gathered while chunk
+    # j + 1 computes; the run table is built by chunk 0 only (PFAAI_FLAG_KEEP_RUNS)
+    nch = max(1, args.chunks)
+    slots = max(1, args.slots) if args.slots else (1 if world == 1 else 2)
     sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
     counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
-    pg = PipelinedGather(counts, dst=0, device=dev)
+    pg = PipelinedGather(counts, dst=0, device=dev, slots=slots)
     stream = torch.cuda.current_stream(dev)
     # pfaai_run indexes by the global JAC index: chunk j writes its own buffer
-    bases = [pg.bufs[j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
+    bases = [[pg.slot_bufs[k][j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
+             for k in range(slots)]
+    n_steps = [0]
 
     def step():
+        i = n_steps[0]
+        n_steps[0] += 1
+        pg.begin(i)  # buffer set i % slots: the stream waits for the gathers that last read it
         for j, (c0, c1) in enumerate(sub[rank]):
             if c1 > c0:
-                eng.run(c0, c1, _capi.FLAG_KEEP_RUNS if j else 0, bases[j], stream=stream.cuda_stream)
+                eng.run(c0, c1, _capi.FLAG_KEEP_RUNS if j else 0, bases[i % slots][j], stream=stream.cuda_stream)
             pg.issue(j)
-        pg.wait()
+        if slots == 1:
+            pg.wait()
 
     def barrier():
         if world > 1:
@@ -225,11 +239,12 @@ def main():
     n_events = 0
     for j, (c0, c1) in enumerate(sub[rank]):
         if c1 > c0:
-            eng.run(c0, c1, 0, bases[j], stream=stream.cuda_stream)
+            eng.run(c0, c1, 0, bases[0][j], stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
             n_events += eng.stats()["n_events"]
     for _ in range(args.warmup):
         step()
+    pg.wait()
     torch.cuda.synchronize(dev)
     barrier()
     eng.timing(reset=True)
@@ -239,6 +254,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    pg.wait()  # every step's gather has landed on rank 0
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
@@ -303,6 +319,7 @@ def main():
                        "genomes": args.genomes, "proteins": args.prot, "pairs": n_pairs, "F": n_f,
                        "events": total_events, "events_per_s": round(total_events / (ms_per_step * 1e-3), 1),
                        "parallelism": f"rowblock{world}",
+                       "gather_pipeline": {"chunks_per_step": nch, "buffer_sets": slots},
                        "hot_path_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                        "k_rows_ms_max_rank": round(k_rows_ms_max, 4),
                        "k_build_ms_max_rank": round(k_build_ms_max, 4)},

@@ -65,12 +65,19 @@ class PipelinedGather:
     j + 1 (RCCL runs on its own stream, ordered after the work already on
     the current stream when issue() is called).
 
+    slots > 1 pipelines across steps as well: step i computes into buffer set
+    i % slots while the gather of step i - 1 is still in flight; begin(i)
+    first makes the current stream wait for the gathers that last read set
+    i % slots (so a rank never overwrites a block RCCL is still sending).
+    Every step still computes and gathers its whole block; wait() drains
+    every outstanding gather.
+
     counts[r][j]: JAC entries of rank r's chunk j.  Because rank blocks and
     their chunks are contiguous row ranges in row order, and rows map to
     contiguous, increasing JAC spans (all-vs-all, QT), the concatenation
     over (r, j) of the received chunks is the full JAC-ordered vector."""
 
-    def __init__(self, counts, dst=0, device=None, dtype=None, group=None):
+    def __init__(self, counts, dst=0, device=None, dtype=None, group=None, slots=1):
         import torch
         import torch.distributed as dist
 
@@ -80,35 +87,56 @@ class PipelinedGather:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.dst = dst
         self.counts = counts
+        self.slots = max(1, int(slots))
         nchunks = len(counts[0])
         dtype = dtype or torch.float64
-        self.bufs = [torch.zeros(max(1, max(c[j] for c in counts)), dtype=dtype, device=device)
-                     for j in range(nchunks)]
-        self.recv = ([[torch.empty_like(b) for _ in range(self.world)] for b in self.bufs]
-                     if (self.world > 1 and self.rank == dst) else None)
-        self.works = []
+        self.slot_bufs = [[torch.zeros(max(1, max(c[j] for c in counts)), dtype=dtype, device=device)
+                           for j in range(nchunks)] for _ in range(self.slots)]
+        self.slot_recv = [([[torch.empty_like(b) for _ in range(self.world)] for b in bufs]
+                           if (self.world > 1 and self.rank == dst) else None) for bufs in self.slot_bufs]
+        self.slot_works = [[] for _ in range(self.slots)]
+        self.cur = 0
+
+    @property
+    def bufs(self):
+        """The current step's chunk buffers."""
+        return self.slot_bufs[self.cur]
+
+    def begin(self, step):
+        """Select buffer set step % slots; its previous gathers must have read it."""
+        self.cur = step % self.slots
+        for w in self.slot_works[self.cur]:
+            w.wait()
+        self.slot_works[self.cur] = []
 
     def issue(self, j):
         if self.world == 1:
             return
-        self.works.append(self.dist.gather(self.bufs[j], self.recv[j] if self.recv else None, dst=self.dst,
-                                           group=self.group, async_op=True))
+        recv = self.slot_recv[self.cur]
+        self.slot_works[self.cur].append(
+            self.dist.gather(self.slot_bufs[self.cur][j], recv[j] if recv else None, dst=self.dst,
+                             group=self.group, async_op=True))
 
     def wait(self):
-        for w in self.works:
-            w.wait()
-        self.works = []
+        for works in self.slot_works:
+            for w in works:
+                w.wait()
+        self.slot_works = [[] for _ in range(self.slots)]
 
-    def result(self):
-        """The full vector on dst (after wait()), None elsewhere."""
+    def result(self, slot=None):
+        """The full vector of buffer set `slot` (default: the current one) on
+        dst (after wait()), None elsewhere."""
         import torch
 
+        k = self.cur if slot is None else slot
+        bufs = self.slot_bufs[k]
         if self.world == 1:
-            return torch.cat([b[: self.counts[0][j]] for j, b in enumerate(self.bufs)])
+            return torch.cat([b[: self.counts[0][j]] for j, b in enumerate(bufs)])
         if self.rank != self.dst:
             return None
-        return torch.cat([self.recv[j][r][: self.counts[r][j]]
-                          for r in range(self.world) for j in range(len(self.bufs))])
+        recv = self.slot_recv[k]
+        return torch.cat([recv[j][r][: self.counts[r][j]]
+                          for r in range(self.world) for j in range(len(bufs))])
 
 
 def gather_rows(out_local, counts, dst=0, group=None):

@@ -88,7 +88,7 @@ def test_gloo_world2_gather_equals_single():
     assert q.get(timeout=10) is True
 
 
-def _pipe_worker(rank, world, port, n, chunks, result_q):
+def _pipe_worker(rank, world, port, n, chunks, slots, steps, result_q):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -101,26 +101,41 @@ def _pipe_worker(rank, world, port, n, chunks, result_q):
     blocks = split_rows(n, world)
     sub = [split_range(b0, b1, chunks, n) for b0, b1 in blocks]
     counts = [[base(c1) - base(c0) for c0, c1 in s] for s in sub]
-    pg = PipelinedGather(counts, dst=0)
-    for j, (c0, c1) in enumerate(sub[rank]):  # "compute" chunk j: its JAC indices
-        pg.bufs[j][: counts[rank][j]] = torch.arange(base(c0), base(c1), dtype=torch.float64)
-        pg.issue(j)
+    pg = PipelinedGather(counts, dst=0, slots=slots)
+    ok = True
+    for step in range(steps):  # step i's "result": JAC index + i, buffer set i % slots
+        pg.begin(step)
+        for j, (c0, c1) in enumerate(sub[rank]):  # "compute" chunk j: its JAC indices
+            pg.bufs[j][: counts[rank][j]] = torch.arange(base(c0), base(c1), dtype=torch.float64) + step
+            pg.issue(j)
+        if step >= slots - 1 and step % 2:  # drain now and then, as bench.py does only at the end
+            pg.wait()
+            full = pg.result()
+            if rank == 0:
+                ok = ok and bool(torch.equal(full, torch.arange(n * (n - 1) // 2, dtype=torch.float64) + step))
     pg.wait()
-    full = pg.result()
+    for k in range(slots):  # the last step that used each buffer set
+        last = max(i for i in range(steps) if i % slots == k)
+        full = pg.result(k)
+        if rank == 0:
+            ok = ok and bool(torch.equal(full, torch.arange(n * (n - 1) // 2, dtype=torch.float64) + last))
     if rank == 0:
-        result_q.put(bool(torch.equal(full, torch.arange(n * (n - 1) // 2, dtype=torch.float64))))
+        result_q.put(ok)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 3), (3, 1)])
-def test_gloo_pipelined_gather_covers_jac_order(world, chunks):
-    """bench.py's N > 1 step: rank blocks cut into pipeline chunks, each chunk
-    gathered asynchronously as soon as it is computed; rank 0's concatenation
-    is the full JAC-ordered vector."""
+@pytest.mark.parametrize("world,chunks,slots,steps", [(2, 3, 1, 1), (3, 1, 1, 1), (2, 1, 2, 5), (3, 2, 2, 4)])
+def test_gloo_pipelined_gather_covers_jac_order(world, chunks, slots, steps):
+    """bench.py's N > 1 steps: rank blocks (optionally cut into pipeline
+    chunks) gathered asynchronously as soon as they are computed, double-
+    buffered across steps (slots = 2: step i + 1 computes while step i's
+    gather is in flight); rank 0's concatenation is each step's full
+    JAC-ordered vector."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, 157, chunks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, 157, chunks, slots, steps, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
