@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--slots", type=int, default=None,
                     help="AJI buffer sets per rank: 2 (default at N > 1) lets step i + 1 compute while "
                          "step i's gather is in flight; 1 waits for each step's gather")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="one-GPU box rehearsal of the N > 1 flow (split, spans, pipelined gather, reassembly, "
+                         "result check): gloo instead of RCCL, every rank on device local %% device_count, the "
+                         "gather through host buffers -- not a measurement")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     args = ap.parse_args()
@@ -179,10 +183,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    rehearse = args.rehearse_gloo and world > 1
+    if rehearse:  # (RCCL refuses two ranks on one device; gloo gathers host tensors)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    hdev = torch.device("cpu") if rehearse else dev  # where the gathered blocks and reductions live
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from parfastaai_amd import _capi, syn
     from parfastaai_amd.datastruct import ParFAAIData
@@ -213,10 +224,12 @@ def main():
     slots = max(1, args.slots) if args.slots else (1 if world == 1 else 2)
     sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
     counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
-    pg = PipelinedGather(counts, dst=0, device=dev, slots=slots)
+    pg = PipelinedGather(counts, dst=0, device=hdev, slots=slots)
     stream = torch.cuda.current_stream(dev)
     # pfaai_run indexes by the global JAC index: chunk j writes its own buffer
-    bases = [[pg.slot_bufs[k][j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
+    # (rehearsal: a device twin of each host gather buffer)
+    dbufs = [[torch.zeros_like(b, device=dev) for b in bs] for bs in pg.slot_bufs] if rehearse else pg.slot_bufs
+    bases = [[dbufs[k][j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
              for k in range(slots)]
     n_steps = [0]
 
@@ -227,13 +240,18 @@ def main():
         for j, (c0, c1) in enumerate(sub[rank]):
             if c1 > c0:
                 eng.run(c0, c1, _capi.FLAG_KEEP_RUNS if j else 0, bases[i % slots][j], stream=stream.cuda_stream)
+            if rehearse:
+                pg.bufs[j].copy_(dbufs[i % slots][j])
             pg.issue(j)
         if slots == 1:
             pg.wait()
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if rehearse:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
 
     # |E| of this rank's rows: one untimed pass, chunk by chunk
     n_events = 0
@@ -263,13 +281,13 @@ def main():
     # per step: the rank's k_blk (once) and its k_rows_pl launches (one per chunk)
     n_runs = args.steps
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=hdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        ev = torch.tensor([n_events], dtype=torch.int64, device=dev)
+        ev = torch.tensor([n_events], dtype=torch.int64, device=hdev)
         dist.all_reduce(ev)
         total_events = int(ev.item())
-        km = torch.tensor([ms_rows / max(n_runs, 1), ms_build / max(n_runs, 1)], dtype=torch.float64, device=dev)
+        km = torch.tensor([ms_rows / max(n_runs, 1), ms_build / max(n_runs, 1)], dtype=torch.float64, device=hdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         k_rows_ms_max, k_build_ms_max = km.tolist()
     else:
@@ -283,6 +301,13 @@ def main():
         vals = pg.result()
         vmin, vmax = float(vals.min().item()), float(vals.max().item())
         assert vals.numel() == n_pairs and 0.0 <= vmin and vmax <= 1.0, (vals.numel(), vmin, vmax)
+        if world > 1:  # the gathered row blocks equal one run over all rows on this device, bit for bit
+            full = torch.empty(n_pairs, dtype=torch.float64, device=dev)
+            eng.run(0, n_rows, 0, full.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            assert torch.equal(full.to(vals.device), vals), "gathered AJI differs from a single-device run"
+            del full
+            log("gathered AJI equals a single-device run over all rows (bit-exact)")
 
         k_rows_ms = ms_rows / max(n_runs, 1)  # rank 0's own k_rows launch(es) per step
         rank_pairs = count
@@ -326,6 +351,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if rehearse:
+            line["rehearsal"] = "gloo, all ranks on one GPU, gather through host memory: flow check, not a measurement"
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
