@@ -170,30 +170,51 @@ class ParFAAIHipImpl {
 
     // algorithm_impl.hpp:281-306
     int computeJAC() {
-        m_JAC = m_ds.initJAC();
-        if (m_mode == PFAAI_MODE_QT && !m_compat) {
-            // correct QT ids = the E ids (query nT + q, target t); SURVEY 8a row Q
-            const int64_t nT = m_ds.tgtSetSize();
-            for (std::size_t i = 0; i < m_JAC.size(); ++i) {
-                m_JAC[i].genomeA = static_cast<IdType>(nT + (int64_t)i / nT);
-                m_JAC[i].genomeB = static_cast<IdType>((int64_t)i % nT);
-            }
-        }
-        const std::size_t n = m_JAC.size();
-        std::vector<double> S(n);
-        std::vector<int32_t> N(n);
+        // the reference's own initJAC (the genome ids of every pair) runs on
+        // a host thread while the device computes S / N / AJI
+        int64_t rows = 0, pairs = 0;
+        pfaai_shape(ctx(), &rows, &pairs);
+        const std::size_t n = (std::size_t)pairs;
+        std::unique_ptr<double[]> S(new double[n ? n : 1]);  // no value-initialisation: the device fills them
+        std::unique_ptr<int32_t[]> N(new int32_t[n ? n : 1]);
         m_AJIdev.resize(n);
         const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
-        if (m_ctx.size() == 1) {
-            int rc = pfaai_compute(ctx(), flags, m_AJIdev.data(), S.data(), N.data());
-            if (rc) throw HipError(rc, pfaai_last_error(ctx()));
-        } else {
-            computeMulti(flags, S.data(), N.data());
+        std::thread ids;
+        bool ids_async = true;
+        try {
+            ids = std::thread([this] { m_JAC = m_ds.initJAC(); });
+        } catch (const std::system_error&) {
+            ids_async = false;
+            m_JAC = m_ds.initJAC();
         }
-        for (std::size_t i = 0; i < n; ++i) {
-            m_JAC[i].S = S[i];
-            m_JAC[i].N = N[i];
+        int rc = PFAAI_RC_OK;
+        std::string err;
+        try {
+            if (m_ctx.size() == 1) {
+                rc = pfaai_compute(ctx(), flags, m_AJIdev.data(), S.get(), N.get());
+                if (rc) err = pfaai_last_error(ctx());
+            } else {
+                computeMulti(flags, S.get(), N.get());
+            }
+        } catch (...) {
+            if (ids_async) ids.join();
+            throw;
         }
+        if (ids_async) ids.join();
+        if (rc) throw HipError(rc, err);
+        if (m_JAC.size() != n) throw HipError(PFAAI_RC_INVALID, "initJAC size differs from the engine's pair count");
+        const bool qt_ids = m_mode == PFAAI_MODE_QT && !m_compat;
+        const int64_t nT = m_ds.tgtSetSize();
+        detail::par_range((int64_t)n, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; ++i) {
+                if (qt_ids) {  // correct QT ids = the E ids (query nT + q, target t); SURVEY 8a row Q
+                    m_JAC[i].genomeA = static_cast<IdType>(nT + i / nT);
+                    m_JAC[i].genomeB = static_cast<IdType>(i % nT);
+                }
+                m_JAC[i].S = S[i];
+                m_JAC[i].N = N[i];
+            }
+        });
         if (m_ctx.size() == 1) {
             pfaai_last_stats(ctx(), &m_events, &m_msBuild, &m_msRows);
             pfaai_run_info(ctx(), &m_rowsKernel, nullptr);

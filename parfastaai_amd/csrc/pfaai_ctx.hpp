@@ -205,5 +205,7 @@ inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
 template <int MODE>
 void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                  hipStream_t s);
+template <int MODE>
+void preload_rows();  // load the mode's row-kernel code object (pfaai_create)
 
 }  // namespace pfaai_impl

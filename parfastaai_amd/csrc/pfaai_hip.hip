@@ -818,6 +818,18 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
         return rc;
     }
     (void)hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long));
+    // every code object of the library loaded now rather than at the first
+    // launch of one of its kernels (HIP's deferred loading), so no caller's
+    // first run pays it (the CLI creates its first context on a thread during
+    // the SQLite read)
+    {
+        hipFuncAttributes a;
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_blk_end<1024, 1>));
+        preload_rows<0>();
+        preload_rows<1>();
+        preload_rows<2>();
+        preload_rows<kModeFull>();
+    }
     *out = c;
     return PFAAI_RC_OK;
 }

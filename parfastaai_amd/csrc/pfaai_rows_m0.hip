@@ -6,4 +6,5 @@
 namespace pfaai_impl {
 template void launch_rows<0>(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S,
                              int32_t* N, hipStream_t s);
+template void preload_rows<0>();
 }  // namespace pfaai_impl
