@@ -435,6 +435,12 @@ __global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
     // (two 1024-thread workgroups per CU: <= 64 VGPRs)
     extern __shared__ uint32_t ende[];  // [tile][n_prot], tetramer-major
     __shared__ int64_t lp[kBlkEndTileMax + 1];
+    // the tile's tetramer at the start of every 64-entry granule of F: one
+    // LDS read per 8-entry chunk instead of a 6-step binary search (a chain
+    // of dependent LDS reads) -- tiles with more granules (a tetramer held by
+    // most genomes) keep the search
+    constexpr int kGran = 6, kGranMax = 8192;
+    __shared__ uint8_t gtl[kGranMax];
     const int tid = threadIdx.x, lane = tid & 63, P = d.n_prot;
     const int t0 = blockIdx.x * tile;
     const int nt = min(tile, kNTetramers - t0);
@@ -442,6 +448,21 @@ __global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
     if (tid <= nt) lp[tid] = d.Lp[t0 + tid];
     __syncthreads();
     const int64_t S = lp[0], E = lp[nt];
+    auto search = [&](int64_t i) {  // last tl with lp[tl] <= i
+        int lo = 0, hi = nt - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lp[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    };
+    const int64_t G0 = S & ~(int64_t)((1 << kGran) - 1);
+    const int64_t ng = ((E - G0) >> kGran) + 1;
+    const bool gran = ng <= kGranMax;  // uniform
+    if (gran) {
+        for (int64_t g = tid; g < ng; g += NTH) gtl[g] = (uint8_t)search(max(G0 + (g << kGran), S));
+        __syncthreads();
+    }
     // U: 16-B loads per lane in flight before the first is used
     for (int64_t cb = (S & ~(int64_t)7) + (int64_t)tid * 8; cb - (int64_t)lane * 8 < E; cb += (int64_t)U * NTH * 8) {
         uint4 v[U];
@@ -459,12 +480,13 @@ __global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
             if (c0 >= E) continue;
             const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
             const int64_t i0 = max(c0, S);
-            int lo = 0, hi = nt - 1;  // tetramer of entry i0: last tl with lp[tl] <= i0
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (lp[mid] <= i0) lo = mid; else hi = mid - 1;
+            int tl;  // tetramer of entry i0
+            if (gran) {
+                tl = gtl[(i0 - G0) >> kGran];  // the granule start's; a boundary may follow inside it
+                while (tl + 1 < nt && lp[tl + 1] <= i0) ++tl;
+            } else {
+                tl = search(i0);
             }
-            int tl = lo;
             int64_t nb = lp[tl + 1];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
