@@ -41,3 +41,47 @@ def test_row_kernel_variants(engine, syn_problem, variant):
     assert impl.n_events() == ref["n_events"]
     assert np.array_equal(jac["N"], ref["N"]) and np.array_equal(jac["S"], ref["S"])
     assert np.array_equal(impl.getAJI(), ref["AJI"])
+
+
+def _problem_from_triples(n, P, trip):
+    """(protein, genome, tetramer) triples -> the loader's arrays (F by
+    (tetramer, protein, genome), Lp, T[P][n], genome-major G)."""
+    p, g, t = (np.asarray(x, np.int64) for x in trip)
+    o = np.lexsort((g, p, t))
+    Lp = np.zeros(160001, np.int64)
+    np.cumsum(np.bincount(t, minlength=160000), out=Lp[1:])
+    T = np.zeros((P, n), np.int32)
+    np.add.at(T, (p, g), 1)
+    og = np.lexsort((t, p, g))
+    G_off = np.zeros(n * P + 1, np.int64)
+    np.cumsum(np.bincount(g * P + p, minlength=n * P), out=G_off[1:])
+    return dict(mode=0, n_ids=n, n_prot=P, Lp=Lp, F_prot=p[o].astype(np.int32), F_genome=g[o].astype(np.int32),
+                T=T, G_off=G_off, G_tet=t[og].astype(np.int32))
+
+
+def test_run_end_table_heavy_tetramer(engine):
+    """k_blk_end with a tetramer held by every (genome, protein): its tile
+    holds 600 000 F entries, past the granule table's 8 192 x 64, so that
+    tile looks tetramers up by binary search while the others use the table;
+    the all-vs-all rows (G_pos walks over the end table) equal the oracle."""
+    rng = np.random.default_rng(11)
+    n, P = 600, 1000
+    gg, pp = np.meshgrid(np.arange(n), np.arange(P), indexing="ij")
+    ts = np.concatenate([np.full((n, P, 1), 777), rng.integers(0, 160000, (n, P, 3)),
+                         rng.integers(20000, 20040, (n, P, 1))], axis=2)
+    ts.sort(axis=2)
+    keep = np.ones(ts.shape, bool)
+    keep[:, :, 1:] = ts[:, :, 1:] != ts[:, :, :-1]  # a set per (genome, protein)
+    rep = lambda x: np.broadcast_to(x[:, :, None], ts.shape)[keep]  # noqa: E731
+    pb = _problem_from_triples(n, P, (rep(pp), rep(gg), ts[keep]))
+    engine.load(**pb)
+    pr = O.Problem(pb)
+    aji, S, N = engine.compute(0)
+    st = engine.stats()
+    assert st["rows_kernel"] == "pl"
+    assert st["n_events"] == pr.count_e()
+    for a in (0, 1, 299, n - 2):
+        So, No, _ = pr.dense_rows(a, a + 1)
+        b = np.arange(a + 1, n)
+        k = n * a + b - (a + 2) * (a + 1) // 2
+        assert np.array_equal(N[k], No[0, b]) and np.array_equal(S[k], So[0, b]), a
