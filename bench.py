@@ -97,7 +97,7 @@ def c2_reference():
     """The reference's own end-to-end time at BASELINE config C2 (2,000
     genomes, SQLite DB -> CSV), measured beside ours by tools/gpu/e2e_c2.py
     and committed as profiles/r02l_e2e_cli_c2.json."""
-    p = os.path.join(ROOT, "profiles", "r02_e2e_cli_c2.json")
+    p = os.path.join(ROOT, "profiles", "r02l_e2e_cli_c2.json")
     try:
         with open(p) as f:
             d = json.load(f)

@@ -90,7 +90,7 @@ void par_range(int64_t n, Fn fn) {
 // Contiguous row blocks over `parts` devices: cut[0] = 0 .. cut[parts] = n,
 // balanced by the row-cost model of parfastaai_amd/shard.py:split_rows (the
 // same cuts, pinned by tests/test_integration_compile.py): all-vs-all row a
-// costs fixed + width = 1.25 n + (n - 1 - a); QT / QSUB rows are equal.
+// costs fixed + width = 1.0 n + (n - 1 - a); QT / QSUB rows are equal.
 inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
     std::vector<int64_t> cut{0};
     if (!all_vs_all) {
@@ -98,7 +98,7 @@ inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
         cut.push_back(n);
         return cut;
     }
-    const double k = 1.25 * (double)n;  // shard.FIXED_COST_FRACTION
+    const double k = 1.0 * (double)n;  // shard.FIXED_COST_FRACTION
     auto before = [&](int64_t a) { return (double)a * k + (double)a * n - (double)(a * (a + 1) / 2); };
     const double total = before(n);
     for (int r = 1; r < parts; ++r) {

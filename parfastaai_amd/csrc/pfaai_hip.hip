@@ -272,7 +272,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         const char* wv = getenv("PFAAI_PL_WINDOWS");
         c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
                      !(wv && wv[0] == '0') &&
-                     (int64_t)c->max_cols + 1 > wcols;
+                     (int64_t)c->cols_run + 1 > wcols;
         if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 80 KB of LDS (nwin * P <= 5120)
             nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
             win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * (int64_t)c->prob.n_prot * nwin));
@@ -943,6 +943,16 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // target set; QT rows already are full rows
     const bool full = (flags & PFAAI_FLAG_FULL_ROWS) && c->prob.mode != PFAAI_MODE_QT;
     c->cols_run = full ? c->prob.n_ids : c->max_cols;
+    // all-vs-all row a has n - 1 - a columns, so a launch is as wide as its
+    // first row: row blocks past the first (a multi-GPU rank's shard, a
+    // stream tile) get the counter words per thread (KW) and column chunks
+    // their own rows need -- fewer T loads and S5 words per protein (the last
+    // 10k/8 shard: 1.36 -> 1.22 ms at KW 1).  PFAAI_PL_LAUNCH_COLS=0 keeps the
+    // problem's widest row (A/B; results identical)
+    if (!full && c->prob.mode == PFAAI_MODE_ALL) {
+        const char* lc = getenv("PFAAI_PL_LAUNCH_COLS");
+        if (!(lc && lc[0] == '0')) c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - rb);
+    }
     if (rb == re) return PFAAI_RC_OK;
     if (full) return run_mode<kModeFull>(c, rb, re, flags, aji, S, N, s);
     switch (c->prob.mode) {

@@ -14,11 +14,14 @@ from __future__ import annotations
 # genome's full G lists (P protein iterations, each a latency chain with one
 # workgroup barrier) whatever its width, then pays per column.  Fitted on
 # MI355X at 10k x 100 SCPs from the 8-way shard times of candidate splits
-# (tools/gpu/shard_times.py, SHARD_FRACS; profiles/r02g_shard_times_10k_x8.txt):
+# (tools/gpu/shard_times.py, SHARD_FRACS): with one KW for every launch,
 # fixed = 0.75 n -> slowest shard 1.45 ms, 1.0 n -> 1.36, 1.25 n -> 1.32,
-# 1.5 n -> 1.33, 2.0 n -> 1.43 (mean 1.26).  Balancing by pairs alone gives
-# the last rank (narrow rows) 2.7 ms.
-FIXED_COST_FRACTION = 1.25
+# 1.5 n -> 1.33, 2.0 n -> 1.43 (profiles/r02g_shard_times_10k_x8.txt); since
+# each launch takes the counter words its own widest row needs, narrow
+# shards got cheaper: 1.25 n -> 1.37, 1.0 n -> 1.29, 1.5 n -> 1.34
+# (profiles/r02m_shard_times_10k_x8.txt).  Balancing by pairs alone gives
+# the last rank (narrow rows) 2.5 ms.
+FIXED_COST_FRACTION = 1.0
 
 
 def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: float | None = None):

@@ -64,7 +64,7 @@ def test_split_rows_balanced():
         blocks = split_rows(n, w)
         assert blocks[0][0] == 0 and blocks[-1][1] == n
         assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
-        k = 1.25 * n  # shard.FIXED_COST_FRACTION
+        k = 1.0 * n  # shard.FIXED_COST_FRACTION
         cost = [sum(k + n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
         if n >= 100 * w:
             assert max(cost) - min(cost) <= 2 * (k + n)  # within a row or two
