@@ -504,5 +504,15 @@ int main(int argc, char** argv) {  // main.cpp:337-356
         rc = parallel_qry2tgt_fastaai(app);
     }
     std::printf("Total (CLI)         : %10.2f ms  (engine teardown included)\n", ms_since(t_main));
+    // Every output file is closed and every engine context destroyed (both
+    // inside the total above); what is left is the HIP runtime's exit-time
+    // teardown of its own state.  Flush and leave without it, unless
+    // PFAAI_CLI_FAST_EXIT=0.
+    const char* fe = std::getenv("PFAAI_CLI_FAST_EXIT");
+    if (!(fe && fe[0] == '0')) {
+        warm_gpu_join();
+        std::fflush(nullptr);
+        std::_Exit(rc);
+    }
     return rc;
 }
