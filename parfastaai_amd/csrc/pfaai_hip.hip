@@ -294,12 +294,17 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
             // A/B: 6.0 -> 2.9 ms at QT 50 000 x 1 000)
             const size_t lds = (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4);
             const char* bt = getenv("PFAAI_BLK_THREADS");
+            // query-vs-target rows' column window IS the table's window: the
+            // row kernel never prunes by splitters there, so they are not built
+            // (k_blk phase 2 off; PFAAI_BLK_QT_SPLIT=1 builds them, A/B)
+            const char* qs = getenv("PFAAI_BLK_QT_SPLIT");
+            const int ph = MODE == 2 && !(qs && qs[0] == '1') ? 2 : 0;
             if (bt && atoi(bt) == 256)
                 hipLaunchKernelGGL((k_blk<true, 256>), dim3(ceil_div(kNTetramers, win_tile)), dim3(256), lds, s, dw,
-                                   win_tile, 0, (int32_t)wcols, nwin);
+                                   win_tile, ph, (int32_t)wcols, nwin);
             else
                 hipLaunchKernelGGL((k_blk<true, 1024>), dim3(ceil_div(kNTetramers, win_tile)), dim3(1024), lds, s, dw,
-                                   win_tile, 0, (int32_t)wcols, nwin);
+                                   win_tile, ph, (int32_t)wcols, nwin);
             if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
                 const int rcf = launch_first_key(c, s);
                 if (rcf) return rcf;

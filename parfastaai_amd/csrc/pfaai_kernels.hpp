@@ -287,7 +287,8 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer for many proteins)
 constexpr int kBlkLdsBytes = 80 << 10;  // its LDS staging: n_prot x tile x 16 B (two workgroups share a CU's 160 KB)
 
-// dbg (diagnostics, PFAAI_BLK_ABLATE): bit 0 skips (1), bit 1 (2), bit 2 (3).
+// dbg: bit 0 skips (1), bit 1 (2), bit 2 (3) -- PFAAI_BLK_ABLATE (diagnostics) and, for
+// query-vs-target window tables, bit 1 (no splitters: nothing there prunes by them).
 // WIN (column windows for rows wider than one row-kernel chunk): one table
 // per absolute column window w = [w * wcols, (w + 1) * wcols), all built in
 // this one pass over F, window-major at blk + w * P * 160000 -- each entry is

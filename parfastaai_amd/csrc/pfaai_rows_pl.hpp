@@ -347,7 +347,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 r = make_uint2(gq2[j] + 1u, r4[j].y);  // OOB entries: (1, 0), empty
                 nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
             } else {
-                nl[j] = run_lines(r4[j], wlo, whi, r, min_len);
+                nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && abs_chunk >= 0));
             }
             rt[st][e] = r;
             if (nl[j] > (uint32_t)kPlMaxLines) {

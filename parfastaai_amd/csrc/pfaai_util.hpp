@@ -41,12 +41,15 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 // min_len: a full run of one member is A alone (no partner), so runs of
 // length <= 1 are skipped; a column-window sub-run (k_blk<true>) may omit A,
 // and one member is then a partner (min_len 0).
-__device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi, uint2& r, uint32_t min_len = 1u) {
+// split = false: the entry's splitter fields were not built (query-vs-target
+// window tables: the row's column window is the table's window, nothing to prune).
+__device__ __forceinline__ uint32_t run_lines(uint4 r4, int32_t wlo, int32_t whi, uint2& r, uint32_t min_len = 1u,
+                                              bool split = true) {
     r = make_uint2(r4.x, r4.y);
     if (r.y - r.x <= min_len) return 0u;
     const uint32_t first = r.x & ~(uint32_t)(kGroup - 1);
     uint32_t nl = (r.y - first + kGroup - 1) / kGroup;
-    if (nl > 1u) {
+    if (split && nl > 1u) {
         const uint64_t sp = (uint64_t)r4.z | ((uint64_t)r4.w << 32);
         uint32_t l0 = 0, l1 = nl;
 #pragma unroll
