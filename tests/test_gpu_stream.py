@@ -214,3 +214,26 @@ def test_compute_rows_two_contexts_fill_one_array(engine):
         assert np.array_equal(a, ref_a) and np.array_equal(S, ref_S) and np.array_equal(N, ref_N)
     finally:
         e2.close()
+
+
+@pytest.mark.timeout(600)
+def test_stream_tiles_switch_window_and_end_table(engine):
+    """All-vs-all, 11 000 genomes (G_pos built): rows wider than one 10 240-
+    column chunk run by column windows over window tables, the later rows in
+    one chunk over the u32 run-end table -- each launch takes its own width,
+    so streamed tiles switch table kinds within one load (PFAAI_FLAG_KEEP_RUNS
+    must not hand a tile the other kind).  Equal to the single-launch run,
+    which covers every row by windows, and to the oracle on sampled rows."""
+    n, P = 11000, 12
+    pb = _all_problem(n, P)
+    engine.load(**pb)
+    aji, S, N = engine.compute(0)
+    a2, S2, N2, _, nt = _collect(engine, 0, n, 1 << 24, _capi.FLAG_EMIT_JAC)
+    assert nt >= 3
+    assert np.array_equal(a2, aji) and np.array_equal(S2, S) and np.array_equal(N2, N)
+    pr = O.Problem(pb)
+    for a in (0, 700, 900, 5000, n - 2):  # 700: wider than a chunk; 900: not
+        So, No, _ = pr.dense_rows(a, a + 1)
+        b = np.arange(a + 1, n)
+        k = n * a + b - (a + 2) * (a + 1) // 2
+        assert np.array_equal(N[k], No[0, b]) and np.array_equal(S[k], So[0, b]), a
