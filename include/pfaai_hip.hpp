@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <exception>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -181,8 +182,15 @@ class ParFAAIHipImpl {
         const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
         std::thread ids;
         bool ids_async = true;
+        std::exception_ptr ids_err;  // initJAC's exception, rethrown on this thread
         try {
-            ids = std::thread([this] { m_JAC = m_ds.initJAC(); });
+            ids = std::thread([this, &ids_err] {
+                try {
+                    m_JAC = m_ds.initJAC();
+                } catch (...) {
+                    ids_err = std::current_exception();
+                }
+            });
         } catch (const std::system_error&) {
             ids_async = false;
             m_JAC = m_ds.initJAC();
@@ -201,6 +209,7 @@ class ParFAAIHipImpl {
             throw;
         }
         if (ids_async) ids.join();
+        if (ids_err) std::rethrow_exception(ids_err);
         if (rc) throw HipError(rc, err);
         if (m_JAC.size() != n) throw HipError(PFAAI_RC_INVALID, "initJAC size differs from the engine's pair count");
         const bool qt_ids = m_mode == PFAAI_MODE_QT && !m_compat;
