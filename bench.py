@@ -96,12 +96,12 @@ def host_info(threads):
 def c2_reference():
     """The reference's own end-to-end time at BASELINE config C2 (2,000
     genomes, SQLite DB -> CSV), measured beside ours by tools/gpu/e2e_c2.py
-    and committed as profiles/r02l_e2e_cli_c2.json."""
-    p = os.path.join(ROOT, "profiles", "r02l_e2e_cli_c2.json")
+    and committed as profiles/r02n_e2e_cli_c2.json."""
+    p = os.path.join(ROOT, "profiles", "r02n_e2e_cli_c2.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return {"source": "profiles/r02l_e2e_cli_c2.json", "genomes": d["genomes"],
+        return {"source": "profiles/r02n_e2e_cli_c2.json", "genomes": d["genomes"],
                 "reference_wall_s": d["reference_wall_s"], "reference_threads": d["reference_threads"],
                 "ours_wall_s": d["ours_wall_s"], "csv_byte_identical": d["csv_byte_identical"]}
     except (OSError, KeyError, ValueError):
