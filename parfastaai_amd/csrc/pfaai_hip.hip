@@ -952,9 +952,12 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // first row: row blocks past the first (a multi-GPU rank's shard, a
     // stream tile) get the counter words per thread (KW) and column chunks
     // their own rows need -- fewer T loads and S5 words per protein (the last
-    // 10k/8 shard: 1.36 -> 1.22 ms at KW 1).  PFAAI_PL_LAUNCH_COLS=0 keeps the
-    // problem's widest row (A/B; results identical)
-    if (!full && c->prob.mode == PFAAI_MODE_ALL) {
+    // 10k/8 shard: 1.36 -> 1.22 ms at KW 1).  Only with G_pos (<= 20 480
+    // genomes), whose run walks start at the row genome: without it a narrow
+    // launch would leave the column windows for whole-run walks pruned by
+    // three splitters (100k streamed: 613 -> 689 ms).  PFAAI_PL_LAUNCH_COLS=0
+    // keeps the problem's widest row (A/B; results identical)
+    if (!full && c->prob.mode == PFAAI_MODE_ALL && c->dev.G_pos) {
         const char* lc = getenv("PFAAI_PL_LAUNCH_COLS");
         if (!(lc && lc[0] == '0')) c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - rb);
     }

@@ -445,9 +445,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             for (int k = 0; k < KW; ++k) {
                 const int32_t w = tid + k * NT;
                 // words past the row's last column stay 0: a wave whose words
-                // are all past it stops (VAR bit 512: no skip, A/B); read and
-                // clear by one ds_wrxchg_rtn_b32: no faster
-                if ((VAR & 512) == 0 && wbase + k * NT >= ncw) break;
+                // are all past it stops (WK 3 only, where row widths vary
+                // within a launch; in the other forms it costs 6 spilled VGPRs
+                // -- 100k streamed 613 -> 689 ms; VAR bit 512: no skip, A/B);
+                // read and clear by one ds_wrxchg_rtn_b32: no faster
+                if (WK == 3 && (VAR & 512) == 0 && wbase + k * NT >= ncw) break;
                 const uint32_t v = acc_p[w];
                 if (v) {
                     acc_p[w] = 0u;
