@@ -2,7 +2,8 @@
 """bench.py -- all-pairs AJI matrix fill on MI355X (BASELINE.json metric).
 
     python bench.py --gpus N --steps K --warmup W
-    (N > 1: launched by torch.distributed.run, one rank per GPU)
+    (N > 1: one rank per GPU -- under torch.distributed.run, or, started
+    plainly, bench.py spawns its own N rank processes before any GPU call)
 
 Workload (BASELINE.json metric "10k-genome all-vs-all"): a synthetic
 10,000-genome x 100-SCP database (SURVEY.md §8d SYN generator, seed
@@ -45,8 +46,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (first: one HIP runtime per process)
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
@@ -154,6 +153,51 @@ def cpu_baseline(sample_genomes=320, n_prot=100):
                       f"{dt:.2f} s", "host": host_info(1), "c2_end_to_end": c2_reference()}
 
 
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`python bench.py --gpus N` (N > 1) started without a launcher: start N
+    child processes of this script, rank r on GPU r (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment),
+    and return the worst exit code.  The parent never touches the GPU (it has
+    not even imported torch) and replaces no process: the children are
+    ordinary subprocesses.  If one rank fails, the others are stopped."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PFAAI_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):  # a rank died: the others would wait at a collective forever
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    try:
+                        rcs[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[r] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"rank exit codes {rcs}")
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,13 +220,27 @@ def main():
                          "gather through host buffers -- not a measurement")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank prints its RANK / WORLD_SIZE / LOCAL_RANK "
+                         "as one JSON line and exits before any GPU call")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: spawn the N ranks here, before anything touches the GPU
+        return spawn_ranks(args.gpus, sys.argv[1:])
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if world != args.gpus:  # never measure a different number of GPUs than asked for
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return 2
+    if args.launch_dry_run:
+        print(json.dumps({"rank": rank, "world_size": world, "local_rank": local,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return 0
+    import torch  # (first: one HIP runtime per process)
+    import torch.distributed as dist
+
     rehearse = args.rehearse_gloo and world > 1
     if rehearse:  # (RCCL refuses two ranks on one device; gloo gathers host tensors)
         local = local % max(1, torch.cuda.device_count())
@@ -194,6 +252,9 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        if rank == 0:
+            ver = ".".join(map(str, torch.cuda.nccl.version())) if not rehearse else "-"
+            log(f"communicator: backend {dist.get_backend()} (RCCL {ver}), size {dist.get_world_size()}")
 
     from parfastaai_amd import _capi, syn
     from parfastaai_amd.datastruct import ParFAAIData
@@ -306,8 +367,14 @@ def main():
             eng.run(0, n_rows, 0, full.data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
             assert torch.equal(full.to(vals.device), vals), "gathered AJI differs from a single-device run"
+            # the other buffer set of the double-buffered gather (the step before the last)
+            checked = [pg.cur]
+            if slots > 1 and args.steps + args.warmup >= 2:
+                k = (n_steps[0] - 2) % slots
+                assert torch.equal(full.to(vals.device), pg.result(slot=k)), f"gathered AJI of buffer set {k} differs"
+                checked.append(k)
             del full
-            log("gathered AJI equals a single-device run over all rows (bit-exact)")
+            log(f"gathered AJI (buffer sets {checked}) equals a single-device run over all rows (bit-exact)")
 
         k_rows_ms = ms_rows / max(n_runs, 1)  # rank 0's own k_rows launch(es) per step
         rank_pairs = count
@@ -360,4 +427,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -18,6 +18,9 @@ except Exception:  # pragma: no cover - torch is optional for the binding
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PFAAI_HIP_LIB", os.path.join(_HERE, "lib", "libpfaai_hip.so"))
+# the same engine built with -DPFAAI_DIAGNOSTICS: the A/B switches (PFAAI_ROWS_KERNEL,
+# PFAAI_PL_WINDOWS, ...) and k_rows_v2 exist only here (tests of the variants, tools/gpu)
+DIAG_LIB_PATH = os.path.join(_HERE, "lib", "libpfaai_hip_diag.so")
 
 NTETRAMERS = 160000
 PFAAI_OK = 0
@@ -66,17 +69,18 @@ class Problem(ctypes.Structure):
     ]
 
 
-_lib = None
+_libs = {}
 
 
-def load_library():
-    """Load libpfaai_hip.so (raises if it was not built: no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"libpfaai_hip.so not found at {LIB_PATH}; run __graft_entry__.build()")
-    lib = ctypes.CDLL(LIB_PATH)
+def load_library(path=None):
+    """Load libpfaai_hip.so, or the library at `path` (e.g. DIAG_LIB_PATH);
+    raises if it was not built: no fallback."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{os.path.basename(path)} not found at {path}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
     vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
     P64 = ctypes.POINTER(ctypes.c_int64)
     sig = {
@@ -111,7 +115,7 @@ def load_library():
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -122,8 +126,8 @@ def _ptr(a):
 class Engine:
     """One pfaai_ctx = one device.  Owns the device-resident problem."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
+    def __init__(self, device: int = 0, lib_path=None):
+        self.lib = load_library(lib_path)
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pfaai_create(ctypes.byref(self.ctx), int(device))
         if rc != PFAAI_OK:

@@ -18,7 +18,10 @@
 
 #include "pfaai_hip.h"
 #include "pfaai_kernels.hpp"
-#include "pfaai_rows_v2.hpp"  // kernel constants (kPlEntries, kV2Threads, kClkBlocks); templates only
+#include "pfaai_rows_pl.hpp"  // kernel constants (kPlEntries, kClkBlocks); templates only
+#ifdef PFAAI_DIAGNOSTICS
+#include "pfaai_rows_v2.hpp"  // k_rows_v2 (A/B only): built into libpfaai_hip_diag.so alone
+#endif
 
 // Diagnostic switches that change results or instrument the kernels
 // (PFAAI_ABLATE, PFAAI_BLK_ABLATE: skip kernel phases; PFAAI_PL_CLK: stage
@@ -185,8 +188,10 @@ inline int pick_kw(int32_t max_cols, int kw_max) {
 // k_rows_pl's chunk width for this problem (launch_rows' KW choice)
 inline int64_t pl_chunk_cols(pfaai_ctx* c) {
     if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->cols_run, 10);
+#ifdef PFAAI_DIAGNOSTICS
     if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->cols_run, 5);
-    const char* km = getenv("PFAAI_PL_KWMAX");
+#endif
+    const char* km = DIAG_ENV("PFAAI_PL_KWMAX");
     return 2 * 1024 * (int64_t)pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 }
 

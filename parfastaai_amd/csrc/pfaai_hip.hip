@@ -174,11 +174,11 @@ int launch_first_key(pfaai_ctx* c, hipStream_t s) {
 template <int MODE>
 int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
     if (ends) {  // k_rows_pl WK 3 reads run ends only (pl_uses_ends)
-        const char* et = getenv("PFAAI_BLK_END_TILE");  // tetramers per workgroup (A/B)
+        const char* et = DIAG_ENV("PFAAI_BLK_END_TILE");  // tetramers per workgroup (A/B)
         const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(et ? std::min(atoi(et), kBlkEndTileMax) : kBlkEndTileMax,
                                                                      kBlkLdsBytes / (4 * c->prob.n_prot)));
         const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint32_t);
-        const char* eu = getenv("PFAAI_BLK_END_U");  // loads in flight per lane (A/B)
+        const char* eu = DIAG_ENV("PFAAI_BLK_END_U");  // loads in flight per lane (A/B)
         const int u = eu ? atoi(eu) : 1;
         if (u >= 4)
             hipLaunchKernelGGL((k_blk_end<1024, 4>), dim3(ceil_div(kNTetramers, tile)), dim3(1024), lds, s, c->dev, tile);
@@ -198,7 +198,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
     // 1024 threads (0.649 vs 0.666 ms at 10k; the window form gains 2x, see
     // run_mode); PFAAI_BLK_THREADS=256 for A/B
-    const char* bt = getenv("PFAAI_BLK_THREADS");
+    const char* bt = DIAG_ENV("PFAAI_BLK_THREADS");
     if (bt && atoi(bt) == 256)
         hipLaunchKernelGGL((k_blk<false, kTetraThreads>), dim3(ceil_div(kNTetramers, tile)), dim3(kTetraThreads), lds, s,
                            c->dev, tile, dbg, 0, 1);
@@ -269,7 +269,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     int win_tile = 0, nwin = 1;
     const int64_t wcols = pl_chunk_cols(c);
     {
-        const char* wv = getenv("PFAAI_PL_WINDOWS");
+        const char* wv = DIAG_ENV("PFAAI_PL_WINDOWS");
         c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
                      !(wv && wv[0] == '0') &&
                      (int64_t)c->cols_run + 1 > wcols;
@@ -293,11 +293,11 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
             // CU, so a 256-thread form ran 8 waves per CU (PFAAI_BLK_THREADS=256
             // A/B: 6.0 -> 2.9 ms at QT 50 000 x 1 000)
             const size_t lds = (size_t)nwin * c->prob.n_prot * win_tile * sizeof(uint4);
-            const char* bt = getenv("PFAAI_BLK_THREADS");
+            const char* bt = DIAG_ENV("PFAAI_BLK_THREADS");
             // query-vs-target rows' column window IS the table's window: the
             // row kernel never prunes by splitters there, so they are not built
             // (k_blk phase 2 off; PFAAI_BLK_QT_SPLIT=1 builds them, A/B)
-            const char* qs = getenv("PFAAI_BLK_QT_SPLIT");
+            const char* qs = DIAG_ENV("PFAAI_BLK_QT_SPLIT");
             const int ph = MODE == 2 && !(qs && qs[0] == '1') ? 2 : 0;
             if (bt && atoi(bt) == 256)
                 hipLaunchKernelGGL((k_blk<true, 256>), dim3(ceil_div(kNTetramers, win_tile)), dim3(256), lds, s, dw,
@@ -911,10 +911,12 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // row kernel: default by input, PFAAI_ROWS_KERNEL overrides (A/B runs)
     {
         int k = !c->has_g ? RK_WORKLIST : c->max_glen > kPlEntries ? RK_FUSED : RK_PL;
-        if (const char* v = getenv("PFAAI_ROWS_KERNEL")) {
+        if (const char* v = DIAG_ENV("PFAAI_ROWS_KERNEL")) {
             const std::string x(v);
             if (x == "pl") k = RK_PL;
+#ifdef PFAAI_DIAGNOSTICS
             else if (x == "v2") k = RK_V2;
+#endif
             else if (x == "pl512") k = RK_PL512;
             else if (x == "fused") k = RK_FUSED;
             else if (x == "worklist") k = RK_WORKLIST;
@@ -928,7 +930,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         c->rows_kernel = k;
     }
     {  // consecutive rows per XCD (L2 sharing of a clade's runs); PFAAI_XCD_CHUNK for A/B
-        const char* xc = getenv("PFAAI_XCD_CHUNK");
+        const char* xc = DIAG_ENV("PFAAI_XCD_CHUNK");
         c->dev.xcd_chunk = xc ? std::max(1, atoi(xc)) : kXcdChunk;
     }
     if (const char* abl = DIAG_ENV("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
@@ -936,7 +938,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33
     // ms at 10k, tools/gpu/ab_rows.py); PFAAI_PL_PRIO=0..3 overrides (A/B)
     {
-        const char* pr = getenv("PFAAI_PL_PRIO");
+        const char* pr = DIAG_ENV("PFAAI_PL_PRIO");
         flags = (flags & ~(3u << 16)) | (uint32_t)((pr ? atoi(pr) : 3) & 3) << 16;
     }
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
@@ -958,7 +960,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // three splitters (100k streamed: 613 -> 689 ms).  PFAAI_PL_LAUNCH_COLS=0
     // keeps the problem's widest row (A/B; results identical)
     if (!full && c->prob.mode == PFAAI_MODE_ALL && c->dev.G_pos) {
-        const char* lc = getenv("PFAAI_PL_LAUNCH_COLS");
+        const char* lc = DIAG_ENV("PFAAI_PL_LAUNCH_COLS");
         if (!(lc && lc[0] == '0')) c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - rb);
     }
     if (rb == re) return PFAAI_RC_OK;
@@ -1307,7 +1309,8 @@ static int stream_matrix_impl(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile
     const bool rot = qt && (flags & PFAAI_FLAG_REF_COMPAT);
     if (rot && c->prob.n_qry > c->prob.n_tgt)
         return fail(c, PFAAI_RC_INVALID,
-                    "pfaai_stream_matrix: the reference's QT ids overlap rows when nQ > nT; use the default ids");
+                    "pfaai_stream_matrix: the reference's QT ids overlap rows when nQ > nT; run without "
+                    "PFAAI_FLAG_REF_COMPAT (CLI: --corrected)");
     const int64_t shift = rot ? c->prob.n_qry % n_cols : 0;
     tile_rows = std::max<int64_t>(1, std::min<int64_t>(tile_rows, re - rb));
     const int64_t ntiles = ceil_div(re - rb, tile_rows);

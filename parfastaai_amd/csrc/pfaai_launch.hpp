@@ -5,7 +5,9 @@
 #pragma once
 #include "pfaai_ctx.hpp"
 #include "pfaai_rows_pl.hpp"
+#ifdef PFAAI_DIAGNOSTICS
 #include "pfaai_rows_v2.hpp"
+#endif
 
 namespace pfaai_impl {
 
@@ -19,7 +21,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
                        (((size_t)c->prob.n_prot + 1) / 2) * sizeof(uint32_t);  // + T[p][A] (u16)
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
-    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || DIAG_ENV("PFAAI_PL_BIGF");
     // member window test (k_rows_pl WK): one chunk per row reaches the last
     // id, so all-vs-all rows test only b > a and -q / full rows test nothing
     constexpr int kWk1 = MODE == 0 ? 1 : MODE == 2 ? 0 : 2;
@@ -63,6 +65,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     }
 }
 
+#ifdef PFAAI_DIAGNOSTICS
 // k_rows_v2 (pfaai_rows_v2.hpp): one 1024-thread workgroup per CU, same
 // chunk and column-window rules as launch_pl
 template <int MODE, int KW>
@@ -72,7 +75,7 @@ void launch_v2(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
     const size_t lds = (4 * (size_t)KW * kV2Threads + c->prob.n_prot + 1) * sizeof(uint32_t);  // u32 counters x 2
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || getenv("PFAAI_PL_BIGF");
+    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || DIAG_ENV("PFAAI_PL_BIGF");
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #ifdef PFAAI_DIAGNOSTICS
         if (KW == 5 && !bigf && DIAG_ENV("PFAAI_V2_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
@@ -105,6 +108,8 @@ void launch_v2(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     }
 }
 
+#endif
+
 template <int MODE, int KW>
 void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                    hipStream_t s) {
@@ -130,6 +135,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
 #define KR_CASE(K) \
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
     if constexpr (MODE != kModeFull) {  // full rows: k_rows_pl / fused only
+#ifdef PFAAI_DIAGNOSTICS
         if (c->rows_kernel == RK_V2) {
             switch (pick_kw<kV2Threads>(c->cols_run, 5)) {
                 case 1: launch_v2<MODE, 1>(c, rb, re, flags, aji, S, N, s); break;
@@ -140,6 +146,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             }
             return;
         }
+#endif
         if (c->rows_kernel == RK_PL512) {
             switch (pick_kw<512>(c->cols_run, 10)) {
                 PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
@@ -150,7 +157,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         }
     }
     if (c->rows_kernel == RK_PL || (MODE == kModeFull && c->rows_kernel != RK_FUSED)) {
-        const char* km = getenv("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
+        const char* km = DIAG_ENV("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 #ifdef PFAAI_DIAGNOSTICS
         if (MODE == 0 && kw == 5 && !c->windows && c->prob.n_prot <= 255 && DIAG_ENV("PFAAI_PL_CLK") &&
@@ -187,7 +194,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
-        const bool nl = c->prob.n_prot <= 255 && !getenv("PFAAI_PL_NREG");
+        const bool nl = c->prob.n_prot <= 255 && !DIAG_ENV("PFAAI_PL_NREG");
         if (nl) {
             switch (kw) {
                 case 1: launch_pl<MODE, 1, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;

@@ -2,16 +2,20 @@
 // (src/main.cpp:56-356) on the MI355X engine.
 //
 //   par_fastaai_amd [-r query_db] [-s sep] [-q query_list] in_db out_csv
-//                   [--ref-compat] [--device N] [--bin PREFIX]
+//                   [--corrected] [--device N] [--bin PREFIX]
 //
 // Ingest reads the `<p>_genomes` blobs (genome-major lists G) and pfaai_load
 // builds F on the device (stable radix sort), so the run takes the
 // benchmarked k_blk + k_rows_pl path; `--loader tetras` reads F from the
 // `<p>_tetras` tables instead (the reference's own F; G is then built on the
-// device).  Default semantics are the corrected ones:
-// a pair sharing no tetramer gets AJI 0, and -r divides by the query's and
-// the target's own tetramer counts; --ref-compat reproduces the reference's
-// values for those cells bit for bit.  Every other cell is identical.
+// device).  The default output is the reference's, byte for byte, quirks
+// included (a pair sharing no tetramer gets the J of
+// E[0]'s protein, algorithm_impl.hpp:90-91; -r divides by T[p][i/nT] +
+// T[p][nQ + i%nT], ds_impl.hpp:434-436) -- the same default as the C++
+// adapter's drop-in constructor.  --corrected opts into the corrected values
+// for those cells (AJI 0; the query's and the target's own counts); every
+// other cell is identical either way.  (--ref-compat, the default, is still
+// accepted.)
 //
 // Same options, same mode dispatch (main.cpp:337-356), same validation
 // errors and exit codes (3 for a bad -q list or overlapping -r genomes,
@@ -48,7 +52,7 @@ struct AppParams {  // main.cpp:56-131
     std::string outFieldSeparator = ",";
     std::string binPrefix;
     std::vector<std::string> qryGenomeSet;
-    bool refCompat = false;
+    bool refCompat = true;  // reference-exact by default (--corrected clears it)
     int device = 0;
     std::string dumpPrefix;    // --dump-arrays: write the loader's Lc/F/T (cereal) and exit (no GPU)
     std::string formatSelftest;  // --format-selftest FILE: print fmt-formatted doubles (hex input)
@@ -98,9 +102,11 @@ const char* kUsage =
     "  -r,--query_db TEXT:FILE  Path to the Query Database [Optional (default: Same as the Input DB)]\n"
     "  -s,--separator TEXT [,]  Field Separator in the output file [Optional (default: ,)].\n"
     "  -q,--query_subset TEXT:FILE  Path to Query List (Should be subset of genomoes in the input DB.)\n"
-    "  --ref-compat             Reproduce the reference's values where it has quirks: pairs sharing no\n"
-    "                           tetramer (default: AJI 0) and -r denominators (default: the query's and\n"
-    "                           the target's own counts).  All other cells are identical either way.\n"
+    "  --corrected              Correct the reference's quirks instead of reproducing them (the default\n"
+    "                           output is par_fastaai.x's, byte for byte): pairs sharing no tetramer get\n"
+    "                           AJI 0, and -r divides by the query's and the target's own tetramer counts.\n"
+    "                           All other cells are identical either way.\n"
+    "  --ref-compat             Reproduce the reference's values (the default)\n"
     "  --loader TEXT [genomes]  genomes: read <p>_genomes, F built on the GPU; tetras: read <p>_tetras\n"
     "  --device INT [0]         HIP device\n"
     "  --devices LIST           Comma-separated HIP devices: rows split over them (all-vs-all, -r)\n"
@@ -141,6 +147,8 @@ int parse(int argc, char** argv, AppParams& a) {
             if (!value(a.pathToQrySubsetFile)) { std::cerr << "--query_subset: 1 required TEXT:FILE missing\n"; return 114; }
         } else if (s == "--ref-compat") {
             a.refCompat = true;
+        } else if (s == "--corrected") {
+            a.refCompat = false;
         } else if (is("--device", "--device")) {
             std::string v;
             if (!value(v)) return 114;

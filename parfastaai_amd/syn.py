@@ -135,6 +135,46 @@ def write_db(path, n_genomes, n_prot=100, genome_prefix="syn", **kw) -> dict:
     return g
 
 
+def write_db_sets(path, sets, n_genomes, n_prot, genome_prefix="syn"):
+    """A FastAAI-schema SQLite DB from explicit memberships: sets[(genome,
+    protein)] = the genome's tetramer ids in that protein (any order; stored
+    sorted).  Same tables and row orders as write_db (for hand-built cases
+    such as pairs that share no tetramer)."""
+    if os.path.exists(path):
+        os.remove(path)
+    T = np.zeros((n_prot, n_genomes), np.int64)
+    for (gi, p), ts in sets.items():
+        T[p, gi] = len(set(ts))
+    con = sqlite3.connect(path)
+    gnames = genome_names(n_genomes, genome_prefix)
+    pnames = protein_names(n_prot)
+    con.execute("CREATE TABLE 'genome_metadata' (genome_name TEXT, genome_id INTEGER PRIMARY KEY, "
+                "genome_length INTEGER, genome_class INTEGER, SCP_count INTEGER)")
+    con.execute("CREATE TABLE 'scp_data' (genome_id INTEGER, SCP_acc TEXT, SCP_score REAL, tetra_count INTEGER)")
+    con.executemany("INSERT INTO genome_metadata VALUES (?,?,?,?,?)",
+                    [(gnames[i], i, 0, 0, int((T[:, i] > 0).sum())) for i in range(n_genomes)])
+    con.executemany("INSERT INTO scp_data VALUES (?,?,?,?)",
+                    [(gi, pnames[p], 0.0, int(T[p, gi])) for p in range(n_prot) for gi in range(n_genomes)
+                     if T[p, gi] > 0])
+    for p, acc in enumerate(pnames):
+        con.execute(f"CREATE TABLE '{acc}_tetras' (tetramer INTEGER PRIMARY KEY, genomes BLOB)")
+        con.execute(f"CREATE TABLE '{acc}_genomes' (genome_id INTEGER PRIMARY KEY, tetramers BLOB)")
+        by_t = {}
+        rows = []
+        for gi in range(n_genomes):
+            ts = sorted(set(sets.get((gi, p), ())))
+            if ts:
+                rows.append((gi, np.asarray(ts, "<i4").tobytes()))
+            for t in ts:
+                by_t.setdefault(t, []).append(gi)
+        con.executemany(f"INSERT INTO '{acc}_genomes' VALUES (?,?)", rows)
+        con.executemany(f"INSERT INTO '{acc}_tetras' VALUES (?,?)",
+                        [(t, np.asarray(gs, "<i4").tobytes()) for t, gs in sorted(by_t.items())])
+    con.commit()
+    con.close()
+    return dict(genome_set=gnames, T=T)
+
+
 def qt_merge(gt: dict, gq: dict) -> dict:
     """QT problem arrays from a target and a query SYN DB (generate() dicts)
     joined as the reference's QT loader does (scp_db.hpp:450-528): per

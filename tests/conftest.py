@@ -22,3 +22,14 @@ def engine():
     e = _capi.Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture(scope="session")
+def diag_engine():
+    """A context of the diagnostics build (libpfaai_hip_diag.so): the only
+    library that reads the A/B switches (PFAAI_ROWS_KERNEL, PFAAI_PL_WINDOWS,
+    ...), so the tests that force a kernel variant use it."""
+    from parfastaai_amd import _capi
+    e = _capi.Engine(0, lib_path=_capi.DIAG_LIB_PATH)
+    yield e
+    e.close()

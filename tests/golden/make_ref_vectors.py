@@ -35,7 +35,37 @@ CASES = {
     # reference's column map intact; its T-index quirk is reproduced under
     # ref-compat and pinned here)
     "qt12": ("qt", dict(n_tgt=12, n_qry=12, n_prot=20, clade_size=4)),
+    # explicit memberships (syn.write_db_sets) with pairs that share no
+    # tetramer in any protein: the reference gives them the
+    # J of E[0]'s protein; the drop-in CLI's default must print the same bytes
+    "zero3": ("sets", dict(n_genomes=3, n_prot=2)),
+    "zero30": ("sets", dict(n_genomes=30, n_prot=3)),
 }
+
+
+def sets_for(name):
+    """The memberships {(genome, protein): tetramers} of a "sets" case."""
+    import numpy as np
+
+    if name == "zero3":  # genome 2 shares no tetramer with genome 0 (tests/test_gpu_parity.py::_zero_overlap_ds)
+        blocks = {(5, 0): [0, 1], (9, 0): [1, 2], (11, 1): [0, 1], (20, 1): [2], (30, 0): [0]}
+        out = {}
+        for (t, p), gs in blocks.items():
+            for g in gs:
+                out.setdefault((g, p), []).append(t)
+        return out
+    # zero30: 30 genomes, 3 proteins, 2-4 tetramers each drawn from 60 ids in
+    # three disjoint ranges per genome group, some proteins missing: many
+    # pairs share nothing at all
+    rng = np.random.default_rng(30)
+    out = {}
+    for g in range(30):
+        grp = g % 3
+        for p in range(3):
+            if rng.random() < 0.8:
+                out[(g, p)] = [int(x) for x in rng.choice(np.arange(grp * 20, grp * 20 + 20) + 1000 * p,
+                                                          size=int(rng.integers(2, 5)), replace=False)]
+    return out
 
 
 def run_ref(args, out_csv):
@@ -50,6 +80,8 @@ def main():
         sys.exit("oracle/_ref/par_fastaai.x missing: run oracle/build_ref.sh")
     with tempfile.TemporaryDirectory() as td:
         for name, (kind, kw) in CASES.items():
+            if len(sys.argv) > 1 and name not in sys.argv[1:]:
+                continue
             out = os.path.join(td, name + ".csv")
             if kind == "all":
                 db = os.path.join(td, name + ".db")
@@ -64,6 +96,10 @@ def main():
                 with open(ql, "w") as f:
                     f.write("\n".join(g["genome_set"][i] for i in query) + "\n")
                 run_ref([db, "-q", ql], out)
+            elif kind == "sets":
+                db = os.path.join(td, name + ".db")
+                syn.write_db_sets(db, sets_for(name), **kw)
+                run_ref([db], out)
             else:
                 kw = dict(kw)
                 nT, nQ = kw.pop("n_tgt"), kw.pop("n_qry")

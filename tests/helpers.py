@@ -116,3 +116,30 @@ def _blocks(g):
         for a, b in zip(cut[:-1], cut[1:]):
             out[(int(t), int(ps[a]))] = Fg[s + a:s + b].astype(np.int64)
     return out
+
+
+def sets_problem(sets, n, P):
+    """All-vs-all problem arrays from explicit memberships {(genome, protein):
+    tetramers} (the syn.write_db_sets cases): F by (tetramer, protein, genome),
+    Lp, T[P][n], genome-major G."""
+    trip = sorted({(p, g, t) for (g, p), ts in sets.items() for t in ts})
+    p, g, t = (np.asarray(x, np.int64) for x in zip(*trip))
+    o = np.lexsort((g, p, t))
+    Lp = np.zeros(160001, np.int64)
+    np.cumsum(np.bincount(t, minlength=160000), out=Lp[1:])
+    T = np.zeros((P, n), np.int32)
+    np.add.at(T, (p, g), 1)
+    og = np.lexsort((t, p, g))
+    G_off = np.zeros(n * P + 1, np.int64)
+    np.cumsum(np.bincount(g * P + p, minlength=n * P), out=G_off[1:])
+    return dict(mode=0, n_ids=n, n_prot=P, Lp=Lp, F_prot=p[o].astype(np.int32), F_genome=g[o].astype(np.int32),
+                T=T, G_off=G_off, G_tet=t[og].astype(np.int32))
+
+
+def dense_all(aji, n):
+    """printOutput's dense all-vs-all fill (main.cpp:143-154) of a JAC-order AJI vector."""
+    M = np.zeros((n, n))
+    a, b = np.triu_indices(n, 1)
+    M[a, b] = aji
+    M[b, a] = aji
+    return M

@@ -57,13 +57,22 @@ def test_product_does_not_import_oracle():
                 assert "import oracle" not in txt and "pfaai_oracle" not in txt, f
 
 
+AB_SWITCHES = (b"PFAAI_ROWS_KERNEL", b"PFAAI_XCD_CHUNK", b"PFAAI_PL_PRIO", b"PFAAI_PL_LAUNCH_COLS",
+               b"PFAAI_PL_WINDOWS", b"PFAAI_BLK_THREADS", b"PFAAI_BLK_QT_SPLIT", b"PFAAI_BLK_END_TILE",
+               b"PFAAI_BLK_END_U", b"PFAAI_PL_KWMAX", b"PFAAI_PL_BIGF", b"PFAAI_PL_NREG")
+
+
 def test_release_library_ignores_diagnostic_switches():
-    """The result-changing ablations and the stage-clock instrumentation
-    (PFAAI_ABLATE, PFAAI_BLK_ABLATE, PFAAI_PL_CLK, PFAAI_DIV_NEWTON) exist
-    only in libpfaai_hip_diag.so (-DPFAAI_DIAGNOSTICS): the release library
-    does not even contain their names, so no environment can change its
-    results."""
+    """The result-changing ablations, the stage-clock instrumentation and
+    every A/B kernel switch exist only in libpfaai_hip_diag.so
+    (-DPFAAI_DIAGNOSTICS): the release library does not even contain their
+    names, so no environment can change its kernel choice or results; the
+    rejected k_rows_v2 is compiled into the diagnostics build alone."""
     blob = open(_capi.LIB_PATH, "rb").read()
-    for name in (b"PFAAI_ABLATE", b"PFAAI_BLK_ABLATE", b"PFAAI_PL_CLK", b"PFAAI_DIV_NEWTON"):
+    for name in (b"PFAAI_ABLATE", b"PFAAI_BLK_ABLATE", b"PFAAI_PL_CLK", b"PFAAI_DIV_NEWTON") + AB_SWITCHES:
         assert name not in blob, name
-    assert b"PFAAI_ROWS_KERNEL" in blob  # result-preserving variant switches stay
+    assert b"k_rows_v2" not in blob
+    diag = open(_capi.DIAG_LIB_PATH, "rb").read()
+    for name in AB_SWITCHES:
+        assert name in diag, name
+    assert b"k_rows_v2" in diag

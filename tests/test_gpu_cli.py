@@ -60,8 +60,8 @@ def test_cli_qt_correct_equals_merged_db_block(tmp_path):
     t = unpack(tmp_path, "xdb_subset1.db")
     q = unpack(tmp_path, "xdb_subset2.db")
     c = unpack(tmp_path, "xdb_subset_combo12.db")
-    run(t, str(tmp_path / "qt.csv"), "-r", q)
-    run(c, str(tmp_path / "all.csv"))
+    run(t, str(tmp_path / "qt.csv"), "-r", q, "--corrected")
+    run(c, str(tmp_path / "all.csv"), "--corrected")
     qr, qc, QM = fm.read_csv_matrix(str(tmp_path / "qt.csv"))
     ar, ac, AM = fm.read_csv_matrix(str(tmp_path / "all.csv"))
     rows = [ar.index(n) for n in qr]
@@ -133,7 +133,7 @@ def test_cli_both_loaders_same_bytes(tmp_path, loader):
     assert np.array_equal(fm.read_vec_f64(str(tmp_path / "b_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
 
 
-@pytest.mark.parametrize("compat", [[], ["--ref-compat"]], ids=["default", "ref-compat"])
+@pytest.mark.parametrize("compat", [[], ["--corrected"]], ids=["default", "corrected"])
 def test_cli_c1_rebuilt_db(tmp_path, compat):
     """Config C1 end to end: the reference's 20-genome DB (rebuilt from its
     fixtures, tests/test_c1_loader.py) through par_fastaai_amd -- CSV byte-
@@ -224,3 +224,29 @@ def test_cli_stream_csv_40k_bounded_rss(tmp_path):
     peak_kb = int(r.stdout.split("PEAK_KB")[1])
     print(r.stdout)
     assert peak_kb < 4_000_000, peak_kb  # < 4 GB, vs 35 GB for the default writer
+
+
+@pytest.mark.parametrize("case", ["zero3", "zero30"])
+def test_cli_default_is_reference_exact_on_zero_overlap(tmp_path, case):
+    """One drop-in default: on DBs whose genome pairs may
+    share no tetramer, `par_fastaai_amd in.db out.csv` prints the reference
+    binary's bytes (the pair gets the J of E[0]'s protein, algorithm_impl.hpp:
+    90-91); --corrected writes AJI 0 for exactly those pairs and the oracle's
+    corrected values everywhere."""
+    import make_ref_vectors as mk
+    import oracle as O
+    from helpers import dense_all, sets_problem
+
+    kw = mk.CASES[case][1]
+    db = str(tmp_path / "z.db")
+    syn.write_db_sets(db, mk.sets_for(case), **kw)
+    out = tmp_path / "out.csv"
+    run(db, str(out))
+    assert out.read_text() == text(f"ref_{case}.csv")
+    run(db, str(out), "--stream-csv", "--tile-rows", "4")
+    assert out.read_text() == text(f"ref_{case}.csv")
+    run(db, str(out), "--corrected")
+    n = kw["n_genomes"]
+    r = O.Problem(sets_problem(mk.sets_for(case), n, kw["n_prot"]), compat=False).ref_run()
+    names = syn.genome_names(n)
+    assert out.read_text() == fm.csv_text(names, names, dense_all(r["AJI"], n))

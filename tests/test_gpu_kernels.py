@@ -1,6 +1,7 @@
 """Kernel-level GPU checks: the row kernels' exact small-integer division is
 bit-identical to IEEE '/', and every selectable row-kernel variant
-(PFAAI_ROWS_KERNEL, read by pfaai_run) reproduces the oracle bit-exactly."""
+(PFAAI_ROWS_KERNEL, read by the diagnostics build's pfaai_run) reproduces the
+oracle bit-exactly; the release build ignores every A/B switch."""
 import os
 
 import numpy as np
@@ -29,16 +30,33 @@ def syn_problem():
 
 
 @pytest.mark.parametrize("variant", ["pl", "v2", "pl512", "fused", "worklist"])
-def test_row_kernel_variants(engine, syn_problem, variant):
+def test_row_kernel_variants(diag_engine, syn_problem, variant):
     ds, ref = syn_problem
     os.environ["PFAAI_ROWS_KERNEL"] = variant
     try:
-        impl = ParFAAIImpl(ds, engine=engine)
+        impl = ParFAAIImpl(ds, engine=diag_engine)
         impl.run()
+        assert impl.engine.stats()["rows_kernel"] == variant
     finally:
         os.environ.pop("PFAAI_ROWS_KERNEL", None)
     jac = impl.getJAC()
     assert impl.n_events() == ref["n_events"]
+    assert np.array_equal(jac["N"], ref["N"]) and np.array_equal(jac["S"], ref["S"])
+    assert np.array_equal(impl.getAJI(), ref["AJI"])
+
+
+def test_release_library_ignores_ab_switches(engine, syn_problem, monkeypatch):
+    """Production kernel choice does not depend on the environment: the
+    release library runs k_rows_pl with a bogus PFAAI_ROWS_KERNEL and a
+    counter-word cap set, and gives the oracle's results."""
+    ds, ref = syn_problem
+    for k, v in (("PFAAI_ROWS_KERNEL", "bogus"), ("PFAAI_PL_KWMAX", "1"), ("PFAAI_PL_WINDOWS", "0"),
+                 ("PFAAI_XCD_CHUNK", "3"), ("PFAAI_PL_PRIO", "0"), ("PFAAI_BLK_END_TILE", "7")):
+        monkeypatch.setenv(k, v)
+    impl = ParFAAIImpl(ds, engine=engine)
+    assert impl.run() == 0
+    assert impl.engine.stats()["rows_kernel"] == "pl"
+    jac = impl.getJAC()
     assert np.array_equal(jac["N"], ref["N"]) and np.array_equal(jac["S"], ref["S"])
     assert np.array_equal(impl.getAJI(), ref["AJI"])
 

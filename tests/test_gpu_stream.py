@@ -158,11 +158,13 @@ def test_f_beyond_2_30_entries(engine):
 
 
 @pytest.mark.parametrize("mode", ["all", "qsub", "qt"])
-def test_column_windows_equal_row_chunks(engine, monkeypatch, mode):
+def test_column_windows_equal_row_chunks(diag_engine, monkeypatch, mode):
     """Rows wider than one k_rows_pl chunk: absolute column windows with a run
     table per window (default) == per-row chunks over one table
-    (PFAAI_PL_WINDOWS=0, itself pinned against the oracle in
-    test_gpu_edges.py), S / N / AJI bit-exact, ref-compat included."""
+    (PFAAI_PL_WINDOWS=0, read by the diagnostics build only; itself pinned
+    against the oracle in test_gpu_edges.py), S / N / AJI bit-exact,
+    ref-compat included."""
+    engine = diag_engine
     if mode == "all":
         pb = _all_problem(21000, 3, clade_size=50, n_random=1)
     elif mode == "qsub":

@@ -113,10 +113,11 @@ def _all_rows(aji, n, r0, r1):
 
 
 @pytest.mark.parametrize("mode", ["all", "qt"])
-def test_stream_matrix_column_windows(engine, monkeypatch, mode):
+def test_stream_matrix_column_windows(diag_engine, monkeypatch, mode):
     """Rows wider than one k_rows_pl chunk (column windows with a run table
     per window) in full-row mode: == the dense fill of pfaai_compute, and ==
-    per-row chunks over one table (PFAAI_PL_WINDOWS=0)."""
+    per-row chunks over one table (PFAAI_PL_WINDOWS=0, diagnostics build)."""
+    engine = diag_engine
     if mode == "all":
         g = syn.generate(21000, 3, clade_size=50, n_random=1)
         ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"]

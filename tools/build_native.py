@@ -2,8 +2,9 @@
 
   hip      parfastaai_amd/lib/libpfaai_hip.so   hipcc --offload-arch=gfx950
   diag     parfastaai_amd/lib/libpfaai_hip_diag.so  the same with -DPFAAI_DIAGNOSTICS
-                                                (ablation / stage-clock switches;
-                                                built only on request: --diag)
+                                                (A/B kernel switches, ablations,
+                                                stage clocks, k_rows_v2; the
+                                                variant tests load it)
   cli      parfastaai_amd/lib/par_fastaai_amd   g++ host CLI over the C ABI
   syn      tools/_build/libpfaai_syn.so         synthetic DB generator
   rebuild  tools/_build/rebuild_xantho_db       C1 DB from the reference's fixtures
@@ -114,7 +115,12 @@ def build_ref(force=False):
 
 
 def build_all(force=False):
-    outs = [build_hip(force), build_syn(force), build_oracle(force), build_cli(force), build_rebuild_tool(force)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=2) as ex:  # the two HIP builds' units compile side by side
+        libs = [ex.submit(build_hip, force), ex.submit(build_hip, force, True)]
+        outs = [f.result() for f in libs]
+    outs += [build_syn(force), build_oracle(force), build_cli(force), build_rebuild_tool(force)]
     try:
         outs.append(build_ref(force))
     except subprocess.CalledProcessError as e:  # the reference build is optional
@@ -124,5 +130,3 @@ def build_all(force=False):
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
-    if "--diag" in sys.argv:
-        build_hip(force="--force" in sys.argv, diag=True)
