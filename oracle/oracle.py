@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "libpfaai_oracle.so")
+LIB = os.environ.get("PFAAI_ORACLE_LIB", os.path.join(HERE, "_build", "libpfaai_oracle.so"))  # (tools/sanitize.py)
 
 
 class Mode(ctypes.Structure):

@@ -14,7 +14,7 @@ from helpers import GOLDEN, gpath, text
 from parfastaai_amd import formats as fm
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLI = os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd")
+CLI = os.environ.get("PFAAI_CLI", os.path.join(ROOT, "parfastaai_amd", "lib", "par_fastaai_amd"))  # (tools/sanitize.py)
 
 
 def run(*args, **kw):
