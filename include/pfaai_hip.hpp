@@ -141,6 +141,21 @@ struct pfaai_mode_of {
     }
 };
 
+// The producer half of the drop-in.  The reference's
+// DataStructInterface::construct() (interface.hpp:306-327) ends with
+// constructE(): the E array of every (protein, genome A, genome B) triple
+// (ds_helper.hpp:362-421) and its comparison sort (psort.hpp:27-53), 86 % of
+// the reference's wall time at C2.  The engine never reads E (refE()), so
+// DeviceE<DS> keeps every other construction step of DS -- the reference's
+// own ParFAAIData / ParFAAIQSubData / ParFAAIQryTgtData, constructors
+// inherited -- and makes constructE() return PFAAI_OK without building it.
+template <class DS>
+class DeviceE : public DS {
+  public:
+    using DS::DS;
+    auto constructE() -> decltype(std::declval<DS&>().constructE()) override { return {}; }
+};
+
 template <typename IdType, typename ValueType, typename DSIT>
 class ParFAAIHipImpl {
   public:

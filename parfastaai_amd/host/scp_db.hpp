@@ -295,6 +295,19 @@ inline int read_genome_lists(Conn& tc, const std::string& schema, const std::str
     });
 }
 
+// Memberships stored in `<schema>.<acc>_tetras` (the reference's F source,
+// scp_db.hpp:161-216): the sum of its blob lengths / 4.  SQLite's length()
+// of a BLOB reads the record header only.  The `<p>_genomes` path is taken
+// only when every protein's genome lists hold exactly as many entries; a
+// DB whose two orientations disagree is read through `<p>_tetras` instead,
+// so the output is the reference's either way.
+inline int64_t tetras_entries(Conn& tc, const std::string& schema, const std::string& acc, int* rc) {
+    int64_t bytes = -1;
+    *rc = tc.each("SELECT TOTAL(length(genomes)) FROM " + schema + "`" + acc + "_tetras`",
+                  [&](sqlite3_stmt* st) { bytes = (int64_t)sqlite3_column_double(st, 0); });
+    return bytes < 0 ? -1 : bytes / 4;
+}
+
 // Sort each list (a blob is normally ascending already) and check that it
 // is a set of valid tetramer ids.  false: a duplicate or an id out of range
 // (the caller falls back to the `<p>_tetras` path, which reads F as stored).
@@ -364,9 +377,14 @@ inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays
                 r.err = 1;
                 continue;
             }
-            const int rc = read_genome_lists(tc, "", meta.proteinSet[p], 0, G, r);
+            int rc = read_genome_lists(tc, "", meta.proteinSet[p], 0, G, r);
             if (rc != SQLITE_OK) r.err = rc;
             if (!r.err) sets[p] = normalise_lists(r);
+            if (!r.err && sets[p]) {  // both orientations hold the same number of memberships
+                const int64_t nt = tetras_entries(tc, "", meta.proteinSet[p], &rc);
+                if (rc != SQLITE_OK) r.err = rc;
+                else sets[p] = nt == (int64_t)r.tet.size();
+            }
         }
     }
     for (int p = 0; p < P; ++p)
@@ -425,9 +443,16 @@ inline int load_qt_g(const std::string& tgt, const std::string& qry, DBMetaData&
                 continue;
             }
             int rc = read_genome_lists(tc, "main.", meta.proteinSet[p], 0, nT, r);
+            const int64_t n_main = (int64_t)r.tet.size();
             if (rc == SQLITE_OK) rc = read_genome_lists(tc, "QueryDB.", meta.proteinSet[p], nT, nQ, r);
             if (rc != SQLITE_OK) r.err = rc;
             if (!r.err) sets[p] = normalise_lists(r);
+            if (!r.err && sets[p]) {  // per DB: both orientations hold the same number of memberships
+                const int64_t nt_main = tetras_entries(tc, "main.", meta.proteinSet[p], &rc);
+                const int64_t nt_qry = rc == SQLITE_OK ? tetras_entries(tc, "QueryDB.", meta.proteinSet[p], &rc) : -1;
+                if (rc != SQLITE_OK) r.err = rc;
+                else sets[p] = nt_main == n_main && nt_qry == (int64_t)r.tet.size() - n_main;
+            }
         }
     }
     for (int p = 0; p < P; ++p)

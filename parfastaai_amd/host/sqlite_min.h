@@ -20,6 +20,7 @@ int sqlite3_bind_text(sqlite3_stmt*, int, const char*, int, void (*)(void*));
 int sqlite3_bind_blob(sqlite3_stmt*, int, const void*, int, void (*)(void*));
 int sqlite3_reset(sqlite3_stmt* pStmt);
 int sqlite3_column_int(sqlite3_stmt*, int iCol);
+double sqlite3_column_double(sqlite3_stmt*, int iCol);
 const void* sqlite3_column_blob(sqlite3_stmt*, int iCol);
 int sqlite3_column_bytes(sqlite3_stmt*, int iCol);
 const unsigned char* sqlite3_column_text(sqlite3_stmt*, int iCol);

@@ -163,3 +163,28 @@ def test_genomes_loader_qt(tmp_path):
     key_q = set(np.unique(tet[F[:, 1] >= nT]).tolist())
     both = np.array([k in key_t and k in key_q for k in tet])
     assert np.array_equal(F[both], ref)
+
+
+def test_genomes_loader_falls_back_when_orientations_disagree(tmp_path):
+    """The `<p>_genomes` ingest is taken only when every protein's genome
+    lists hold as many memberships as its `<p>_tetras` blobs (the reference's
+    F source, scp_db.hpp:161-216); a DB whose two orientations disagree is
+    read through `<p>_tetras`, so the output stays the reference's."""
+    import sqlite3
+
+    from parfastaai_amd import syn
+
+    db = str(tmp_path / "s.db")
+    syn.write_db(db, n_genomes=12, n_prot=4, clade_size=4)
+    r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", str(tmp_path / "g"))
+    assert r.returncode == 0 and "<p>_genomes -> G" in r.stdout, r.stdout + r.stderr
+    con = sqlite3.connect(db)
+    gid, blob = con.execute("SELECT genome_id, tetramers FROM `SYN00002.1_genomes` LIMIT 1").fetchone()
+    t = np.frombuffer(blob, "<i4")
+    extra = next(x for x in range(159999, 0, -1) if x not in set(t.tolist()))  # a tetramer F does not list
+    con.execute("UPDATE `SYN00002.1_genomes` SET tetramers = ? WHERE genome_id = ?",
+                (np.sort(np.r_[t, extra]).astype("<i4").tobytes(), gid))
+    con.commit()
+    con.close()
+    r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", str(tmp_path / "g"))
+    assert r.returncode == 0 and "<p>_tetras -> F" in r.stdout, r.stdout + r.stderr

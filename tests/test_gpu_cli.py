@@ -250,3 +250,26 @@ def test_cli_default_is_reference_exact_on_zero_overlap(tmp_path, case):
     r = O.Problem(sets_problem(mk.sets_for(case), n, kw["n_prot"]), compat=False).ref_run()
     names = syn.genome_names(n)
     assert out.read_text() == fm.csv_text(names, names, dense_all(r["AJI"], n))
+
+
+def test_cli_fast_exit_writes_complete_outputs(tmp_path):
+    """The CLI leaves by std::_Exit after flushing (skipping the HIP
+    runtime's exit-time teardown); every output -- CSV, --bin's three cereal
+    files, --stream-csv, --stream-aji -- must be byte-identical to a run that
+    returns from main normally (PFAAI_CLI_FAST_EXIT=0), with the same exit
+    code."""
+    db = unpack(tmp_path, "xdb_subset1.db")
+    outs = {}
+    for fast in ("1", "0"):
+        d = tmp_path / f"fast{fast}"
+        d.mkdir()
+        env = dict(os.environ, PFAAI_CLI_FAST_EXIT=fast)
+        for args in ([str(d / "a.csv"), "--bin", str(d / "b")], [str(d / "s.csv"), "--stream-csv", "--tile-rows", "3"],
+                     [str(d / "u.csv"), "--stream-aji", str(d / "s_aji.bin")]):
+            r = subprocess.run([CLI, db, *args], capture_output=True, text=True, timeout=300, env=env)
+            outs.setdefault(args[1], []).append(r.returncode)
+        outs[fast] = {f: (d / f).read_bytes() for f in ("a.csv", "b_jac.bin", "b_aji.bin", "b_aji_matrix.bin",
+                                                        "s.csv", "s_aji.bin")}
+    assert outs["1"] == outs["0"]
+    assert all(rc == [0, 0] for k, rc in outs.items() if k not in ("0", "1"))
+    assert outs["1"]["a.csv"].decode() == text("xdb_subset1_aji_matrix_wheader.csv")

@@ -2,11 +2,14 @@
 reference's own headers (CPU only, g++ -fsyntax-only; skipped where
 /root/reference is absent).
 
-  * the documented swap applied to the reference's src/main.cpp (read at
-    test time, never copied into this repository): include pfaai_hip.hpp and
+  * the documented swap (INTEGRATION.md §1's diff, applied by
+    tools/dropin.swap) on the reference's src/main.cpp (read at test time,
+    never copied into this repository): include pfaai_hip.hpp, the three
+    data-structure classes wrapped in pfaai::DeviceE (no E), and
     `using PFImpl = pfaai::ParFAAIHipImpl<IdType, ValueType, PFDSInterface>;`
     -- main.cpp:193, 256, 324 (`PFImpl pfaaiImpl(data)`), 196/260/327
-    (`print_aji`) and printOutput (main.cpp:133-175) then compile unchanged;
+    (`print_aji`) and printOutput (main.cpp:133-175) then compile unchanged
+    (tests/test_gpu_dropin.py runs the linked binary);
   * ParFAAIHipImpl explicitly instantiated (every member) for the three
     reference DSIT classes ParFAAIData / ParFAAIQSubData / ParFAAIQryTgtData
     and for the abstract DefaultDataStructInterface;
@@ -14,8 +17,8 @@ reference's own headers (CPU only, g++ -fsyntax-only; skipped where
     enum PFAAI_ERROR_CODE (interface.hpp:39-44).
 """
 import os
-import re
 import subprocess
+import sys
 
 import pytest
 
@@ -32,20 +35,14 @@ def _flags():
             f"-I{ROOT}/include"]
 
 
-def _integration_swap():
-    """The two lines INTEGRATION.md §1 tells a maintainer to change."""
-    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    inc = re.search(r'^\+(#include "pfaai_hip.hpp".*)$', doc, re.M).group(1)
-    using = re.search(r"^\+(using PFImpl = .*;)\s*$", doc, re.M).group(1)
-    return inc, using
-
-
 def test_integration_swap_compiles_in_reference_main(tmp_path):
-    inc, using = _integration_swap()
-    src = open(MAIN).read()
-    old = "using PFImpl = ParFAAIImpl<IdType, ValueType>;"
-    assert old in src
-    src = src.replace('#include "pfaai/scp_db.hpp"', '#include "pfaai/scp_db.hpp"\n' + inc, 1).replace(old, using)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import dropin
+
+    src = dropin.swap(open(MAIN).read())
+    assert "using PFImpl = pfaai::ParFAAIHipImpl<IdType, ValueType, PFDSInterface>;" in src
+    assert "using PFData = pfaai::DeviceE<ParFAAIData<IdType>>;" in src
+    assert "ParFAAIImpl<IdType, ValueType>" not in src
     f = tmp_path / "main_hip.cpp"
     f.write_text(src)
     r = subprocess.run(_flags() + [str(f)], capture_output=True, text=True)

@@ -12,6 +12,9 @@
   ref      oracle/_ref/par_fastaai.x            the reference, from its own
                                                 sources (only where
                                                 /root/reference exists)
+  dropin   oracle/_ref/par_fastaai_hip.x        the reference's main.cpp with
+                                                INTEGRATION.md §1's swap, linked
+                                                to libpfaai_hip.so (tools/dropin.py)
 Everything is built in-tree so the snapshot that travels to the GPU box
 carries the binaries.
 """
@@ -22,6 +25,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PFAAI_ARCH", "gfx950")
 
@@ -125,6 +129,12 @@ def build_all(force=False):
         outs.append(build_ref(force))
     except subprocess.CalledProcessError as e:  # the reference build is optional
         print(f"reference build failed: {e}", file=sys.stderr)
+    try:  # the reference's main.cpp with INTEGRATION.md §1's swap, over libpfaai_hip.so
+        import dropin
+
+        outs.append(dropin.build(force))
+    except (subprocess.CalledProcessError, RuntimeError) as e:
+        print(f"drop-in build failed: {e}", file=sys.stderr)
     return outs
 
 
