@@ -47,6 +47,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+E2E_PROFILE = "r02n_e2e_cli_c2.json"  # tools/gpu/e2e_c2.py's latest committed run
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
 ROWS_KERNEL = "pfaai::k_rows_pl (fused scatter + Jaccard + AJI, default row kernel)"
@@ -72,10 +73,37 @@ def traffic_from_profiles(genomes, prot, world):
         return None
 
 
+def cgroup_cpus():
+    """CPUs of this process's cgroup CPU quota (cgroup v2 cpu.max / v1
+    cfs_quota), None if unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def host_info(threads):
     """The CPU the baseline ran on: model name, logical CPUs of the machine,
-    CPUs this process may use (the box's cgroup share can be far smaller
-    than nproc), threads the baseline was given."""
+    CPUs this process may run on (affinity), the cgroup's CPU quota (the
+    box's share can be far smaller than both), threads the baseline was
+    given."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -85,66 +113,104 @@ def host_info(threads):
                     break
     except OSError:
         pass
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        usable = None
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "threads_used": threads}
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable_cpus(),
+            "cgroup_cpu_quota": cgroup_cpus(), "threads_used": threads}
 
 
 def c2_reference():
-    """The reference's own end-to-end time at BASELINE config C2 (2,000
-    genomes, SQLite DB -> CSV), measured beside ours by tools/gpu/e2e_c2.py
-    and committed as profiles/r02n_e2e_cli_c2.json."""
-    p = os.path.join(ROOT, "profiles", "r02n_e2e_cli_c2.json")
+    """The end-to-end C2 comparison (2,000 genomes, SQLite DB -> CSV) of our
+    CLI, the reference-side drop-in and the reference, medians of repeated
+    runs by tools/gpu/e2e_c2.py, committed under profiles/."""
+    p = os.path.join(ROOT, "profiles", E2E_PROFILE)
     try:
         with open(p) as f:
             d = json.load(f)
-        return {"source": "profiles/r02n_e2e_cli_c2.json", "genomes": d["genomes"],
+        return {"source": "profiles/" + E2E_PROFILE, "genomes": d["genomes"], "repeats": d.get("repeats", 1),
                 "reference_wall_s": d["reference_wall_s"], "reference_threads": d["reference_threads"],
-                "ours_wall_s": d["ours_wall_s"], "csv_byte_identical": d["csv_byte_identical"]}
+                "ours_wall_s": d["ours_wall_s"], "dropin_wall_s": d.get("dropin_wall_s"),
+                "csv_byte_identical": d["csv_byte_identical"]}
     except (OSError, KeyError, ValueError):
         return None
 
 
-def cpu_baseline(sample_genomes=320, n_prot=100):
-    """Reference CLI on a SYN sample; returns the cpu_baseline object."""
+def run_reference(ref, db, threads, timeout=900):
+    """The reference CLI on one SQLite DB; its own phase timers (interface.hpp:
+    309-325, algorithm_impl.hpp:304).  A heartbeat line every 30 s."""
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as td:
+        p = subprocess.Popen([ref, db, os.path.join(td, "out.csv")], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True, env=env)
+        while True:
+            try:
+                out, _ = p.communicate(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                if time.perf_counter() - t0 > timeout:
+                    p.kill()
+                    raise RuntimeError("reference timed out")
+                log(f"cpu baseline: reference running {time.perf_counter() - t0:.0f}s")
+    wall = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise RuntimeError(f"reference exited {p.returncode}")
+
+    def ms(label):
+        m = re.search(re.escape(label) + r"\s*:\s*([0-9.e+]+) ms", out)
+        return float(m.group(1)) if m else None
+
+    e_ms, jac_ms = ms("E constr.   (fin)"), ms("JAC Construction")
+    return {"hot_s": (e_ms + jac_ms) / 1e3, "e_constr_s": e_ms / 1e3, "jac_s": jac_ms / 1e3, "wall_s": wall}
+
+
+def cpu_baseline(n_prot=100, c2_genomes=2000, sample_genomes=320, quick=False):
+    """The reference CLI (built from its own sources) timed on this host's
+    cores with OMP_NUM_THREADS = the CPUs this process may use (BASELINE.md
+    plan): at config C2 (SYN 2,000 x 100 -- the largest config the reference
+    can run) unless quick, and on the N = 320 sample (secondary field).
+    Hot path = its own 'E constr. (fin)' + 'JAC Construction' timers.  Falls
+    back to the CPU oracle ("port") where the binary is absent."""
     from parfastaai_amd import syn
 
     ref = os.path.join(ROOT, "oracle", "_ref", "par_fastaai.x")
-    threads = min(16, os.cpu_count() or 1)
-    pairs = sample_genomes * (sample_genomes - 1) // 2
-    if os.path.exists(ref):
-        with tempfile.TemporaryDirectory() as td:
-            db = os.path.join(td, "syn.db")
-            syn.write_db(db, sample_genomes, n_prot)
-            env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-            t0 = time.perf_counter()
-            r = subprocess.run([ref, db, os.path.join(td, "out.csv")], capture_output=True, text=True, env=env,
-                               timeout=600)
-            wall = time.perf_counter() - t0
-            if r.returncode != 0:
-                raise RuntimeError(f"reference exited {r.returncode}")
-
-            def ms(label):
-                m = re.search(re.escape(label) + r"\s*:\s*([0-9.e+]+) ms", r.stdout)
-                return float(m.group(1)) if m else None
-
-            e_ms, jac_ms = ms("E constr.   (fin)"), ms("JAC Construction")
-            hot_s = (e_ms + jac_ms) / 1e3
-            return {"value": pairs / hot_s, "unit": "genome-pairs/s", "cores": threads, "kind": "reference",
-                    "sample": f"reference par_fastaai.x (built from its sources) on SYN N={sample_genomes} "
-                              f"P={n_prot} all-vs-all; hot path = its own 'E constr. (fin)' + 'JAC "
-                              f"Construction' timers = {hot_s:.2f} s (wall incl. SQLite+CSV {wall:.1f} s); "
-                              f"OMP_NUM_THREADS={threads}",
-                    "host": host_info(threads), "c2_end_to_end": c2_reference()}
-    # fallback: the CPU oracle (single thread restatement of the reference)
+    threads = usable_cpus()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from parfastaai_amd.datastruct import ParFAAIData
 
-    g = syn.generate(sample_genomes, n_prot)
-    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    def sizes(n):  # |F| and the reference's |E| (countTetramerTuples, ds_helper.hpp:206-265) of SYN n x P
+        g = syn.generate(n, n_prot)
+        ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+        return len(g["F_genome"]), O.Problem(ds.problem()).count_e(), ds
+
+    if os.path.exists(ref):
+        def measure(n):
+            n_f, n_e, _ = sizes(n)
+            pairs = n * (n - 1) // 2
+            with tempfile.TemporaryDirectory() as td:
+                db = os.path.join(td, "syn.db")
+                t0 = time.perf_counter()
+                syn.write_db(db, n, n_prot)
+                log(f"cpu baseline: SYN {n} x {n_prot} DB written in {time.perf_counter() - t0:.1f}s")
+                r = run_reference(ref, db, threads)
+            b_alg = 8 * n_e + 4 * n_f + 8 * pairs  # SURVEY §8d
+            return {"genomes": n, "pairs": pairs, "events": n_e, "F": n_f, "hot_s": round(r["hot_s"], 3),
+                    "e_constr_s": round(r["e_constr_s"], 3), "jac_s": round(r["jac_s"], 3),
+                    "wall_s": round(r["wall_s"], 2), "pairs_per_s": round(pairs / r["hot_s"], 1),
+                    "events_per_s": round(n_e / r["hot_s"], 1), "alg_GBps": round(b_alg / r["hot_s"] / 1e9, 3)}
+
+        small = measure(sample_genomes)
+        main = small if quick else measure(c2_genomes)
+        return {"value": main["pairs_per_s"], "unit": "genome-pairs/s", "cores": threads, "kind": "reference",
+                "sample": f"reference par_fastaai.x (built from its own sources) on SYN N={main['genomes']} "
+                          f"P={n_prot} all-vs-all ({'config C2' if not quick else 'quick sample'}), "
+                          f"OMP_NUM_THREADS={threads} (this process's usable CPUs); hot path = its own "
+                          f"'E constr. (fin)' + 'JAC Construction' timers = {main['hot_s']:.2f} s "
+                          f"(wall incl. SQLite + CSV {main['wall_s']:.1f} s)",
+                "c2": None if quick else main, "secondary_sample": small, "host": host_info(threads),
+                "c2_end_to_end": c2_reference()}
+    # fallback: the CPU oracle (single thread restatement of the reference)
+    n_f, n_e, ds = sizes(sample_genomes)
+    pairs = sample_genomes * (sample_genomes - 1) // 2
     t0 = time.perf_counter()
     O.Problem(ds.problem()).ref_run()
     dt = time.perf_counter() - t0
@@ -205,7 +271,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--genomes", type=int, default=10000)
     ap.add_argument("--prot", type=int, default=100)
-    ap.add_argument("--cpu-baseline", choices=["auto", "none"], default="auto")
+    ap.add_argument("--cpu-baseline", choices=["auto", "quick", "none"], default="auto",
+                    help="auto: the reference at config C2 (~2 min) + the N=320 sample; quick: the sample only")
     ap.add_argument("--cpu-sample", type=int, default=320)
     ap.add_argument("--chunks", type=int, default=1,
                     help="pipeline chunks per rank and step (gather of chunk j overlaps chunk j+1); "
@@ -390,7 +457,7 @@ def main():
         if args.cpu_baseline != "none" and world == 1:
             try:
                 log("cpu baseline ...")
-                cpu = cpu_baseline(args.cpu_sample, args.prot)
+                cpu = cpu_baseline(args.prot, sample_genomes=args.cpu_sample, quick=args.cpu_baseline == "quick")
             except Exception as e:  # reported, never fatal
                 cpu = {"value": None, "error": str(e)}
         line = {
