@@ -93,10 +93,17 @@ def cgroup_cpus():
 
 
 def usable_cpus():
+    """CPUs this process can actually run on: its affinity set, capped by its
+    cgroup CPU quota.  (On the GPU box the affinity lists 256 CPUs but the
+    quota is 16: the reference at 256 OpenMP threads ran C2 in 131.5 s vs
+    112.8 s at 16 -- oversubscribed, its parallel loader phases slowed 3-7x,
+    profiles/r03a_e2e_c2_threads256.json -- so 256 would understate it.)"""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return max(1, min(n, int(q))) if q else n
 
 
 def host_info(threads):
@@ -113,7 +120,11 @@ def host_info(threads):
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable_cpus(),
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "usable_cpus": usable_cpus(),
             "cgroup_cpu_quota": cgroup_cpus(), "threads_used": threads}
 
 
@@ -164,8 +175,8 @@ def run_reference(ref, db, threads, timeout=900):
 
 def cpu_baseline(n_prot=100, c2_genomes=2000, sample_genomes=320, quick=False):
     """The reference CLI (built from its own sources) timed on this host's
-    cores with OMP_NUM_THREADS = the CPUs this process may use (BASELINE.md
-    plan): at config C2 (SYN 2,000 x 100 -- the largest config the reference
+    cores with OMP_NUM_THREADS = the CPUs this process can use (affinity
+    capped by the cgroup quota; BASELINE.md plan): at config C2 (SYN 2,000 x 100 -- the largest config the reference
     can run) unless quick, and on the N = 320 sample (secondary field).
     Hot path = its own 'E constr. (fin)' + 'JAC Construction' timers.  Falls
     back to the CPU oracle ("port") where the binary is absent."""
@@ -203,7 +214,7 @@ def cpu_baseline(n_prot=100, c2_genomes=2000, sample_genomes=320, quick=False):
         return {"value": main["pairs_per_s"], "unit": "genome-pairs/s", "cores": threads, "kind": "reference",
                 "sample": f"reference par_fastaai.x (built from its own sources) on SYN N={main['genomes']} "
                           f"P={n_prot} all-vs-all ({'config C2' if not quick else 'quick sample'}), "
-                          f"OMP_NUM_THREADS={threads} (this process's usable CPUs); hot path = its own "
+                          f"OMP_NUM_THREADS={threads} (this process's usable CPUs: affinity capped by the cgroup quota); hot path = its own "
                           f"'E constr. (fin)' + 'JAC Construction' timers = {main['hot_s']:.2f} s "
                           f"(wall incl. SQLite + CSV {main['wall_s']:.1f} s)",
                 "c2": None if quick else main, "secondary_sample": small, "host": host_info(threads),
@@ -337,8 +348,12 @@ def main():
     eng = _capi.Engine(local)
     t0 = time.perf_counter()
     eng.load(**ds.problem())
+    load_wall_ms = (time.perf_counter() - t0) * 1e3
     del g
-    log(f"pfaai_load (H2D + sizing) {time.perf_counter() - t0:.1f}s")
+    ms_checks, ms_upload, ms_load_dev = eng.load_timing()
+    load_path = eng.load_info()
+    log(f"pfaai_load {load_wall_ms:.0f} ms (host checks {ms_checks:.0f}, H2D {ms_upload:.0f}, device {load_path} "
+        f"{ms_load_dev:.2f} ms)")
     n_rows, n_pairs = eng.shape()
     blocks = split_rows(n_rows, world)
     spans = [eng.row_span(rb, re) for rb, re in blocks]
@@ -381,13 +396,18 @@ def main():
             else:
                 dist.barrier(device_ids=[local])
 
-    # |E| of this rank's rows: one untimed pass, chunk by chunk
+    # |E| of this rank's rows: one untimed pass, chunk by chunk -- also the
+    # one-shot cost: the load's device build + this first step
+    eng.timing(reset=True)
     n_events = 0
     for j, (c0, c1) in enumerate(sub[rank]):
         if c1 > c0:
             eng.run(c0, c1, 0, bases[0][j], stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
             n_events += eng.stats()["n_events"]
+    first_wall_ms = (time.perf_counter() - t0) * 1e3  # since the load began
+    _, fb, fr = eng.timing(reset=True)
+    first_step_ms = fb + fr
     for _ in range(args.warmup):
         step()
     pg.wait()
@@ -453,6 +473,21 @@ def main():
                     "kernel": ROWS_KERNEL,
                     "kernel_ms": round(k_rows_ms, 4), "alg_bytes_per_launch": alg_bytes,
                     "build_kernels_ms": round(ms_build / max(n_runs, 1), 4)}
+        # the one-shot load: the device F / G transposition (SURVEY §8d timed
+        # region starts after it; reported here, never in `value`).  Algorithmic
+        # bytes per F entry of the both-given check (G_CHECKED): read its
+        # (protein, genome) 8 B + the caller's G_tet 4 B, write G_pos 4 B and
+        # the u16 protein column 2 B = 18 B; the two-pass sort moves ~58 B
+        # (pfaai_sort.hpp: per pass a histogram read + a read and a write of
+        # 8-B records)
+        alg_per_f = {"g_checked": 18, "g_from_f": 22, "f_from_g": 22}.get(load_path)
+        load = {"path": load_path, "device_ms": round(ms_load_dev, 3), "host_checks_ms": round(ms_checks, 1),
+                "h2d_ms": round(ms_upload, 1), "wall_ms": round(load_wall_ms, 1), "F": n_f,
+                "alg_bytes_per_F": alg_per_f,
+                "alg_GBps": round(alg_per_f * n_f / (ms_load_dev * 1e-3) / 1e9, 1) if alg_per_f else None,
+                "frac": round(alg_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if alg_per_f else None,
+                "one_shot_ms": round(ms_load_dev + first_step_ms, 3), "first_step_ms": round(first_step_ms, 3),
+                "one_shot_wall_ms": round(first_wall_ms, 1)}
         cpu = None
         if args.cpu_baseline != "none" and world == 1:
             try:
@@ -483,6 +518,7 @@ def main():
                        "k_rows_ms_max_rank": round(k_rows_ms_max, 4),
                        "k_build_ms_max_rank": round(k_build_ms_max, 4)},
             "roofline": roofline,
+            "load": load,
             "cpu_baseline": cpu,
         }
         if rehearse:

@@ -223,9 +223,26 @@ int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
 int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
                        double* h_aji, double* h_S, int32_t* h_N);
 
-/* Wall times (ms) of the last pfaai_load: host-side checks, H2D copies, and
- * the device-side F / G build (or G-covers-F check) up to its completion. */
+/* Times (ms) of the last pfaai_load: host-side checks and H2D copies (wall),
+ * and the device span of the F / G build (or G-covers-F check), HIP events
+ * on the context stream from its first kernel to its last. */
 int pfaai_load_timing(const pfaai_ctx* ctx, double* ms_checks, double* ms_upload, double* ms_device);
+
+/* Which orientation the last pfaai_load built on the device (the
+ * replacement of the reference's F construction, ds_helper.hpp:126-162 /
+ * scp_db.hpp:161-216, and of its G read, scp_db.hpp:219-262):
+ *   AS_GIVEN    nothing built (both given, G a superset of F: QT lists of
+ *               both DBs, checked by search)
+ *   G_CHECKED   both given: one sort of F by (genome, protein) proved G to
+ *               be F's transpose and produced G_pos
+ *   G_FROM_F    F only: G by the same sort (list bounds from T, verified)
+ *   F_FROM_G    G only: F by a two-pass sort of the protein-major G entries
+ *               by tetramer
+ *   LEGACY      the general 8-bit LSD radix sort (inputs whose record fields
+ *               do not fit the transposition sort's 64-bit records) */
+enum { PFAAI_LOAD_AS_GIVEN = 0, PFAAI_LOAD_G_CHECKED = 1, PFAAI_LOAD_G_FROM_F = 2, PFAAI_LOAD_F_FROM_G = 3,
+       PFAAI_LOAD_LEGACY = 4 };
+int pfaai_load_info(const pfaai_ctx* ctx, int32_t* path);
 
 /* Which row kernel the last pfaai_run launched (PFAAI_ROWS_*) and whether it
  * ran by absolute column windows (rows wider than one kernel chunk). */

@@ -38,7 +38,9 @@ EXPORTS = [
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
     "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_load_timing", "pfaai_stream_matrix",
+    "pfaai_load_info",
 ]
+LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
@@ -109,6 +111,7 @@ def load_library(path=None):
         "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pfaai_load_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
+        "pfaai_load_info": (ctypes.c_int, [vp, ctypes.POINTER(i32)]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     }
@@ -283,6 +286,12 @@ class Engine:
         self._check(self.lib.pfaai_load_timing(self.ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
                     "pfaai_load_timing")
         return a.value, b.value, c.value
+
+    def load_info(self):
+        """Which orientation the last load built on the device (LOAD_PATHS)."""
+        k = ctypes.c_int32()
+        self._check(self.lib.pfaai_load_info(self.ctx, ctypes.byref(k)), "pfaai_load_info")
+        return LOAD_PATHS.get(k.value, "?")
 
     def timing(self, reset=True):
         """(n_runs, ms_build_total, ms_rows_total) of the runs since the last reset."""

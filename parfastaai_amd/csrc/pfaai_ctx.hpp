@@ -49,7 +49,8 @@ struct pfaai_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     bool loaded = false;
-    double load_ms[3] = {0, 0, 0};  // last pfaai_load: host checks, H2D uploads, device F/G build (+ sync)
+    double load_ms[3] = {0, 0, 0};  // last pfaai_load: host checks, H2D uploads, device F/G build (HIP events)
+    int32_t load_path = 0;          // PFAAI_LOAD_*: which transposition the last load ran (pfaai_load_info)
 
     // problem (host copies of scalars + small maps)
     pfaai_problem prob{};
@@ -75,6 +76,8 @@ struct pfaai_ctx {
     DevBuf cnt_t, off_t;
     DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
     DevBuf out_aji, out_S, out_N, dbg;
+    DevBuf srec_a, srec_b, shist, sgsum, sbase;  // the load-time transposition sort (pfaai_sort.hpp)
+    hipEvent_t load_ev[2] = {nullptr, nullptr};  // device span of the last load's F / G build
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
     // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers

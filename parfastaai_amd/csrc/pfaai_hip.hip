@@ -19,6 +19,7 @@
 #include "pfaai_aux.hpp"
 #include "pfaai_build.hpp"
 #include "pfaai_ctx.hpp"
+#include "pfaai_sort.hpp"
 
 using namespace pfaai;
 
@@ -441,6 +442,174 @@ void release_sort_space(pfaai_ctx* c) {
     c->wl_ready = false;
 }
 
+// ---- the load-time transposition sort (pfaai_sort.hpp) ---------------------
+// passes and digit width for kb-bit keys: one pass up to 11 bits, two up to
+// 22 (10-bit digits for the 20-bit keys g * P + p at 10k x 100), three above
+int tsort_db(int kb, int* passes) {
+    *passes = kb <= kSortMaxDB ? 1 : kb <= 2 * kSortMaxDB ? 2 : 3;
+    return std::max(8, (kb + *passes - 1) / *passes);
+}
+
+// records ping-pong (srec_b only for keygen sources or three passes), the
+// tile histograms, the group sums, the digit bases
+int ensure_tsort(pfaai_ctx* c, int64_t n, int kb, bool keygen) {
+    int passes;
+    const int db = tsort_db(kb, &passes);
+    const int64_t nn = std::max<int64_t>(n, 1);
+    const int64_t ntiles = ceil_div(nn, kSortTile), ngroups = ceil_div(ntiles, kSortGroup);
+    int rc;
+    if ((rc = ensure(c, c->srec_a, nn * 8)) || ((keygen || passes > 2) && (rc = ensure(c, c->srec_b, nn * 8))) ||
+        (rc = ensure(c, c->shist, (size_t)ntiles * (4u << db))) ||
+        (rc = ensure(c, c->sgsum, (size_t)ngroups * (4u << db))) || (rc = ensure(c, c->sbase, 4u << db)))
+        return rc;
+    return PFAAI_RC_OK;
+}
+
+// exclusive-scan workspace (k_scan_tiles' tile sums) for n values
+int ensure_scan(pfaai_ctx* c, int64_t n) {
+    return ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max<int64_t>(n, PFAAI_NTETRAMERS), kScanTile)) * 8);
+}
+
+template <int DB, class S0, class DN>
+void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int passes, hipStream_t s) {
+    const int64_t ntiles = ceil_div(n, kSortTile), ngroups = ceil_div(ntiles, kSortGroup);
+    auto* hist = static_cast<uint32_t*>(c->shist.p);
+    auto* gsum = static_cast<uint32_t*>(c->sgsum.p);
+    auto* base = static_cast<uint32_t*>(c->sbase.p);
+    uint64_t* buf[2] = {static_cast<uint64_t*>(c->srec_a.p), static_cast<uint64_t*>(c->srec_b.p)};
+    const size_t lds = sort_scatter_lds<DB>();
+    for (int pass = 0; pass < passes; ++pass) {
+        const int shift = pass * DB;
+        const bool last = pass == passes - 1;
+        const SrcRecs prev{buf[(pass + 1) & 1]};  // pass p reads what pass p - 1 wrote
+        const DstRecs next{buf[pass & 1]};
+        if (pass == 0)
+            hipLaunchKernelGGL((k_sort_hist<DB, S0>), dim3(ntiles), dim3(kSortThreads), 0, s, src0, n, shift, hist);
+        else
+            hipLaunchKernelGGL((k_sort_hist<DB, SrcRecs>), dim3(ntiles), dim3(kSortThreads), 0, s, prev, n, shift,
+                               hist);
+        hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
+        hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base);
+#define SC(SRC_T, SRC, DST_T, DST)                                                                        \
+    hipLaunchKernelGGL((k_sort_scatter<DB, SRC_T, DST_T>), dim3(ntiles), dim3(kSortThreads), lds, s, SRC, DST, n, \
+                       shift, hist, gsum, base)
+        if (pass == 0 && last) SC(S0, src0, DN, dstN);
+        else if (pass == 0) SC(S0, src0, DstRecs, next);
+        else if (last) SC(SrcRecs, prev, DN, dstN);
+        else SC(SrcRecs, prev, DstRecs, next);
+#undef SC
+    }
+}
+
+// Stable sort of n records by their low kb bits, src0 -> ... -> dstN.  A
+// keygen source (SrcRecs) must read srec_b: the first pass writes srec_a.
+template <class S0, class DN>
+int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipStream_t s) {
+    if (n == 0) return PFAAI_RC_OK;
+    int passes;
+    switch (tsort_db(kb, &passes)) {
+        case 8: tsort_launch<8>(c, src0, dstN, n, passes, s); break;
+        case 9: tsort_launch<9>(c, src0, dstN, n, passes, s); break;
+        case 10: tsort_launch<10>(c, src0, dstN, n, passes, s); break;
+        default: tsort_launch<11>(c, src0, dstN, n, passes, s); break;
+    }
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_RC_OK;
+}
+
+void release_tsort(pfaai_ctx* c) {
+    for (DevBuf* b : {&c->srec_a, &c->srec_b, &c->shist, &c->sgsum, &c->sbase}) release(*b);
+}
+
+// Both F and G given with |G| = |F|: G must be F's genome-major transpose.
+// One two-pass sort of F by g * P + p proves it against the caller's lists
+// and yields G_pos (and the u16 protein column) on the way (DstGposCheck).
+// Returns -1 on a mismatch.
+int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipStream_t s) {
+    const int kb = bits_for(ng);
+    int rc;
+    if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
+    const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
+                       (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
+    const DstGposCheck dst{want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr,
+                           static_cast<const int32_t*>(c->G_tet.p), static_cast<const int64_t*>(c->G_off.p),
+                           static_cast<const int64_t*>(c->Lp.p), err};
+    if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
+    int bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return bad ? -1 : PFAAI_RC_OK;
+}
+
+// F only: G_off from T (a consistent problem's T[p][g] is the length of list
+// (g, p), A7 / ds_helper.hpp:46-79), then one sort of keygen records (key g *
+// P + p, tetramer and block offset carried) into G_tet / G_pos, every list
+// bound verified (DstGFromF).  Returns -1 if the records do not fit 64 bits
+// or T disagrees with F: the caller takes build_g_from_f.
+int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_pos, hipStream_t s) {
+    const int32_t P = c->prob.n_prot, ni = c->prob.n_ids;
+    const int kb = bits_for(ng);
+    if (kb + 18 + jb > 64) return -1;
+    int rc;
+    if ((rc = ensure_tsort(c, n_f, kb, true)) || (rc = ensure(c, c->G_off, (ng + 1) * 8)) ||
+        (rc = ensure(c, c->G_tet, std::max<int64_t>(n_f, 1) * 4)) || (rc = ensure(c, c->cnt_t, std::max<int64_t>(ng, 1) * 4)) ||
+        (rc = ensure_scan(c, ng)))
+        return rc;
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
+    auto* len = static_cast<uint32_t*>(c->cnt_t.p);
+    hipLaunchKernelGGL(k_len_from_t, dim3((int)std::min<int64_t>(ceil_div(ng, 256), 8192)), dim3(256), 0, s,
+                       static_cast<const int32_t*>(c->T.p), P, ni, c->prob.t_cols, len);
+    if ((rc = scan_u32(c, len, ng, static_cast<unsigned long long*>(c->G_off.p), s))) return rc;
+    hipLaunchKernelGGL(k_fkeys_rec, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
+                       static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), (uint32_t)P, kb,
+                       static_cast<uint64_t*>(c->srec_b.p), static_cast<uint16_t*>(c->Fp16.p));
+    HIPCHK(c, hipGetLastError());
+    const SrcRecs src{static_cast<const uint64_t*>(c->srec_b.p)};
+    const DstGFromF dst{want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr, static_cast<int32_t*>(c->G_tet.p),
+                        static_cast<const int64_t*>(c->G_off.p), static_cast<const int64_t*>(c->Lp.p), kb, err};
+    if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
+    int bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return bad ? -1 : PFAAI_RC_OK;
+}
+
+// G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
+// protein-major (k_gkeys_pm; Lc counted on the way), one two-pass sort by
+// tetramer (18-bit keys, 9-bit digits) -> F (t, p, g), Fp16 and G_pos
+// (DstFFromG).  Needs P < 4096, n_ids < 2^21, lists < 8192 entries (the
+// record fields); else the caller takes build_f_from_g.
+int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, bool want_pos, hipStream_t s) {
+    const int32_t P = c->prob.n_prot, ni = c->prob.n_ids;
+    int rc;
+    if ((rc = ensure_tsort(c, n, 18, true)) || (rc = ensure(c, c->cnt_t, std::max<int64_t>(n_lists, PFAAI_NTETRAMERS) * 4)) ||
+        (rc = ensure(c, c->off_t, (n_lists + 1) * 8)) || (rc = ensure_scan(c, n_lists)))
+        return rc;
+    auto* len = static_cast<uint32_t*>(c->cnt_t.p);
+    auto* pm_off = static_cast<unsigned long long*>(c->off_t.p);
+    hipLaunchKernelGGL(k_len_pm, dim3((int)std::min<int64_t>(ceil_div(n_lists, 256), 8192)), dim3(256), 0, s,
+                       static_cast<const int64_t*>(c->G_off.p), P, ni, len);
+    if ((rc = scan_u32(c, len, n_lists, pm_off, s))) return rc;
+    auto* lc = len;  // the lengths are consumed by the scan (stream order): reuse the buffer for Lc
+    HIPCHK(c, hipMemsetAsync(lc, 0, PFAAI_NTETRAMERS * 4, s));
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n_lists, 4), 1), 1 << 16);
+    hipLaunchKernelGGL(k_gkeys_pm, dim3(grid), dim3(256), 0, s, static_cast<const int64_t*>(c->G_off.p),
+                       static_cast<const int32_t*>(c->G_tet.p), n_lists, P, ni, pm_off,
+                       static_cast<uint64_t*>(c->srec_b.p), lc);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = scan_u32(c, lc, PFAAI_NTETRAMERS, static_cast<unsigned long long*>(c->Lp.p), s))) return rc;
+    const SrcRecs src{static_cast<const uint64_t*>(c->srec_b.p)};
+    const DstFFromG dst{static_cast<int32_t*>(c->Fp.p), static_cast<int32_t*>(c->Fg.p),
+                        static_cast<uint16_t*>(c->Fp16.p), want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr,
+                        static_cast<const int64_t*>(c->G_off.p), (uint32_t)P};
+    return tsort(c, src, dst, n, 18, s);
+}
+
 int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     HIPCHK(c, hipSetDevice(c->device));
     c->loaded = false;
@@ -523,11 +692,14 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     const int64_t n_f = in_f ? p.n_f : n_g;
     if (n_f < 0 || n_f > kMaxF) return fail(c, PFAAI_RC_INVALID, "|F| must be <= 2^32 - 64");
     std::vector<int64_t> fcount(ni, 0);  // F entries per genome (work-list sizes)
+    int64_t max_lc = 0;                  // largest tetramer block of F
     if (in_f) {
         if (p.Lp[0] != 0 || p.Lp[PFAAI_NTETRAMERS] != p.n_f)
             return fail(c, PFAAI_RC_INVALID, "Lp must start at 0 and end at n_f");
-        for (int t = 0; t < PFAAI_NTETRAMERS; ++t)
+        for (int t = 0; t < PFAAI_NTETRAMERS; ++t) {
             if (p.Lp[t + 1] < p.Lp[t]) return fail(c, PFAAI_RC_INVALID, "Lp must be non-decreasing");
+            max_lc = std::max<int64_t>(max_lc, p.Lp[t + 1] - p.Lp[t]);
+        }
         if (in_g && n_g < n_f) return fail(c, PFAAI_RC_INVALID, "G must hold every membership of F (|G| < |F|)");
         std::vector<std::vector<int64_t>> fc(16);
         std::atomic<int> bad_id{0}, bad_p{0}, bad_sort{0};
@@ -684,36 +856,38 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     } else {
         release(c->G_pos);
     }
-    if (!in_f && (rc = build_f_from_g(c, ng, n_f, s))) return rc;
+    const bool want_pos = c->G_pos.p != nullptr;
+    // the u16 protein column (k_blk's run detection): written by the
+    // transposition sorts on the way, else by k_fp16 below
+    if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
+    HIPCHK(c, hipMemsetAsync(c->Fp16.p, 0, (n_f + 16) * sizeof(uint16_t), s));
+    for (hipEvent_t& e : c->load_ev)
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+    HIPCHK(c, hipEventRecord(c->load_ev[0], s));
+    bool fp16_done = false;
+    c->load_path = PFAAI_LOAD_AS_GIVEN;
+    if (!in_f) {  // G only: F (and G_pos) by the transposition sort (record fields permitting)
+        if (P < kMaxRuns && ni < (1 << 21) && c->max_glen < 8192) {
+            if ((rc = build_f_from_g_sorted(c, ng, n_f, want_pos, s))) return rc;
+            fp16_done = true;
+            c->load_path = PFAAI_LOAD_F_FROM_G;
+        } else {
+            if ((rc = build_f_from_g(c, ng, n_f, s))) return rc;
+            c->load_path = PFAAI_LOAD_LEGACY;
+        }
+    }
     pos_ok = !in_f;
     bool has_g = in_g;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
-        // the transpose of F -- build that transpose (the F-only path) and
-        // compare word for word, a sort and a stream instead of a search per entry
-        DevBuf user_off, user_tet;
-        std::swap(user_off, c->G_off);
-        std::swap(user_tet, c->G_tet);
-        rc = build_g_from_f(c, ng, n_f, s);
-        auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-        unsigned long long ne = 0;
-        if (!rc) {
-            HIPCHK(c, hipMemsetAsync(sc + SC_GRAND, 0, sizeof(unsigned long long), s));
-            const int gb = (int)std::min<int64_t>(ceil_div(n_f, 256), 8192);
-            hipLaunchKernelGGL(k_count_ne, dim3(gb), dim3(256), 0, s, static_cast<const uint32_t*>(c->G_tet.p),
-                               static_cast<const uint32_t*>(user_tet.p), n_f, sc + SC_GRAND);
-            hipLaunchKernelGGL(k_count_ne, dim3((int)std::min<int64_t>(ceil_div(2 * (ng + 1), 256), 8192)), dim3(256), 0,
-                               s, static_cast<const uint32_t*>(c->G_off.p), static_cast<const uint32_t*>(user_off.p),
-                               2 * (ng + 1), sc + SC_GRAND);
-            HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipMemcpyAsync(&ne, sc + SC_GRAND, sizeof(ne), hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-        }
-        release(user_off);
-        release(user_tet);
+        // the transpose of F -- one sort of F by (genome, protein) proves it
+        // against the caller's lists (and yields G_pos): no search per entry
+        rc = check_g_transpose(c, ng, n_f, want_pos, s);
+        if (rc == -1)
+            return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
         if (rc) return rc;
-        if (ne) return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
-        pos_ok = true;
+        pos_ok = fp16_done = true;
+        c->load_path = PFAAI_LOAD_G_CHECKED;
     } else if (in_g && in_f && n_f) {  // both given, G larger (QT: both DBs' lists): G must hold F (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
         int* err = reinterpret_cast<int*>(sc + SC_ERR);
@@ -732,11 +906,30 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         if (bad) return fail(c, PFAAI_RC_INVALID, "G lists a membership that F does not hold");
         if ((int64_t)found != n_f) return fail(c, PFAAI_RC_INVALID, "G does not hold every membership of F");
     } else if (!in_g && ng < ((int64_t)1 << 32)) {  // G from F (keys g * P + p fit 32 bits)
-        if ((rc = build_g_from_f(c, ng, n_f, s))) return rc;
-        std::vector<int64_t> goff(ng + 1);
-        HIPCHK(c, hipMemcpyAsync(goff.data(), c->G_off.p, (ng + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, goff[k + 1] - goff[k]);
+        // G_off from T when T counts exactly F's memberships per (genome,
+        // protein) -- then one sort; else (or if any list bound disagrees) the
+        // general radix sort with G_off from the sorted keys
+        int64_t tsum = 0, tmax = 0;
+        for (int64_t q = 0; q < P; ++q)
+            for (int32_t g = 0; g < ni; ++g) {
+                tsum += p.T[q * p.t_cols + g];
+                tmax = std::max<int64_t>(tmax, p.T[q * p.t_cols + g]);
+            }
+        rc = tsum == n_f ? build_g_from_f_sorted(c, ng, n_f, bits_for(max_lc + 1), want_pos, s) : -1;
+        if (rc == -1) {
+            if ((rc = build_g_from_f(c, ng, n_f, s))) return rc;
+            std::vector<int64_t> goff(ng + 1);
+            HIPCHK(c, hipMemcpyAsync(goff.data(), c->G_off.p, (ng + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            for (int64_t k = 0; k < ng; ++k) c->max_glen = std::max<int64_t>(c->max_glen, goff[k + 1] - goff[k]);
+            c->load_path = PFAAI_LOAD_LEGACY;
+        } else if (rc) {
+            return rc;
+        } else {
+            c->max_glen = tmax;
+            fp16_done = true;
+            c->load_path = PFAAI_LOAD_G_FROM_F;
+        }
         has_g = true;
         pos_ok = true;
     }
@@ -746,12 +939,11 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         release(c->G_tet);
     }
     if (!has_g || !pos_ok) release(c->G_pos);
-    if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
-    HIPCHK(c, hipMemsetAsync(c->Fp16.p, 0, (n_f + 16) * sizeof(uint16_t), s));
-    if (n_f)
+    if (n_f && !fp16_done)
         hipLaunchKernelGGL(k_fp16, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 1 << 16)), dim3(256), 0, s,
                            static_cast<const int32_t*>(c->Fp.p), n_f, static_cast<uint16_t*>(c->Fp16.p));
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->load_ev[1], s));
     if (has_g && (rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
 
     Dev& d = c->dev;
@@ -789,8 +981,14 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     const auto t3 = clk::now();
     c->load_ms[0] = ms(t0, t1);
     c->load_ms[1] = ms_upload;
-    c->load_ms[2] = ms(t2, t3);
+    {
+        float dev_ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&dev_ms, c->load_ev[0], c->load_ev[1]));
+        c->load_ms[2] = dev_ms;
+    }
+    (void)t3;
     release_sort_space(c);  // pfaai_run never allocates; the work-list path re-allocates below
+    release_tsort(c);
     if (!has_g && (rc = ensure_worklists(c))) return rc;
     c->loaded = true;
     return PFAAI_RC_OK;
@@ -846,9 +1044,12 @@ int pfaai_destroy(pfaai_ctx* c) {
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
-                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw})
+                      &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw, &c->srec_a, &c->srec_b, &c->shist,
+                      &c->sgsum, &c->sbase})
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->load_ev)
+        if (e) (void)hipEventDestroy(e);
     release(c->st_dev);
     if (c->st_host) (void)hipHostFree(c->st_host);
     for (int i = 0; i < 2; ++i) {
@@ -993,6 +1194,12 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     if (h_S) HIPCHK(c, hipMemcpyAsync(h_S, S, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     if (h_N) HIPCHK(c, hipMemcpyAsync(h_N, N, np * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_RC_OK;
+}
+
+int pfaai_load_info(const pfaai_ctx* c, int32_t* path) {
+    if (!c || !c->loaded) return PFAAI_RC_INVALID;
+    if (path) *path = c->load_path;
     return PFAAI_RC_OK;
 }
 

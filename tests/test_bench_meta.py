@@ -26,7 +26,7 @@ def test_pmc_traffic_profile_present():
 
 def test_host_info_fields():
     h = bench.host_info(16)
-    assert set(h) == {"cpu_model", "nproc", "usable_cpus", "cgroup_cpu_quota", "threads_used"}
+    assert set(h) == {"cpu_model", "nproc", "affinity_cpus", "usable_cpus", "cgroup_cpu_quota", "threads_used"}
     assert h["threads_used"] == 16
 
 

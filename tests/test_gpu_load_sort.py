@@ -1,0 +1,121 @@
+"""The load-time transposition sort (pfaai_sort.hpp):
+F <-> G on the device by a stable LSD radix sort of 64-bit records in one,
+two or three passes of <= 11-bit digits.
+
+  * both orientations given: one sort of F by (genome, protein) must accept
+    exactly the caller's G -- a swapped tetramer or a shifted list bound is
+    refused -- and its G_pos drives the benchmark kernel (WK 3) to the
+    oracle's results;
+  * F only: G_off from T, verified against the sorted keys; an inconsistent
+    T (a count that is not the list length) falls back to the general radix
+    sort, and the results still follow the reference's formula with that T;
+  * G only: F by the protein-major enumeration sorted by tetramer; a list
+    too long for the record fields falls back to the general sort;
+  * key widths that take one, two and three passes, and record counts that
+    are not a multiple of the 8192-record tile -- bit-exact against the
+    oracle and against each other.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from parfastaai_amd import _capi, syn
+from parfastaai_amd.datastruct import ParFAAIData
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(n, P, **kw):
+    g = syn.generate(n, P, **kw)
+    return ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(
+        g["G_off"], g["G_tet"]).problem()
+
+
+def _strip(pb, drop):
+    return {k: v for k, v in pb.items() if k not in drop}
+
+
+def _check_rows(engine, pb, rows, res):
+    aji, S, N = res
+    pr = O.Problem(pb)
+    n = pb["n_ids"]
+    for a in rows:
+        So, No, _ = pr.dense_rows(a, a + 1)
+        b = np.arange(a + 1, n)
+        k = n * a + b - (a + 2) * (a + 1) // 2
+        assert np.array_equal(N[k], No[0, b]) and np.array_equal(S[k], So[0, b]), a
+
+
+@pytest.mark.parametrize("n,P,kw,passes", [
+    (20, 40, dict(clade_size=5), 1),          # g * P + p < 2^11: one pass
+    (701, 37, dict(clade_size=9), 2),          # 15-bit keys, |F| not a multiple of the tile
+    (3000, 1500, dict(clade_size=10, has=0.02), 3),  # 23-bit keys: three 8-bit passes
+])
+def test_orientations_agree_across_pass_counts(engine, n, P, kw, passes):
+    pb = _problem(n, P, **kw)
+    assert (n * P).bit_length() <= 11 * passes
+    results = {}
+    for drop, want in (((), "g_checked"), (("G_off", "G_tet"), "g_from_f"), (("Lp", "F_prot", "F_genome"), "f_from_g")):
+        engine.load(**_strip(pb, drop))
+        assert engine.load_info() == want, drop
+        results[want] = engine.compute(0)
+        assert engine.stats()["n_events"] == O.Problem(pb).count_e()
+    for k in ("g_from_f", "f_from_g"):
+        for a, b in zip(results[k], results["g_checked"]):
+            assert np.array_equal(a, b), k
+    _check_rows(engine, pb, (0, 1, n // 2, n - 2), results["g_checked"])
+
+
+def test_both_given_refuses_a_g_that_is_not_the_transpose(engine):
+    pb = _problem(300, 24, clade_size=10)
+    G_off, G_tet = pb["G_off"], pb["G_tet"]
+    # (1) one tetramer of one list replaced by another id (still an ascending set)
+    bad = G_tet.copy()
+    k0, k1 = int(G_off[5 * 24 + 3]), int(G_off[5 * 24 + 4])
+    lst = set(bad[k0:k1].tolist())
+    new = next(t for t in range(159999, 0, -1) if t not in lst)
+    bad[k0:k1] = np.sort(np.r_[bad[k0:k1 - 1], new])
+    with pytest.raises(_capi.PfaaiError):
+        engine.load(**dict(pb, G_tet=bad))
+    # (2) one entry moved from a list to its neighbour: same |G|, same G_tet, shifted bound
+    off = G_off.copy()
+    j = next(j for j in range(1000, len(off) - 1) if off[j + 1] - off[j] > 1 and off[j] - off[j - 1] > 1)
+    off[j] += 1
+    with pytest.raises(_capi.PfaaiError):
+        engine.load(**dict(pb, G_off=off))
+    engine.load(**pb)  # the real transpose is accepted
+    assert engine.load_info() == "g_checked"
+
+
+def test_f_only_inconsistent_t_takes_the_general_sort(engine):
+    """T is an input of the formula (J = c / (T[p][A] + T[p][B] - c)); when it
+    is not the list lengths of F, G_off cannot come from it: the general
+    radix sort builds G, and S / N follow the reference with that T."""
+    pb = _strip(_problem(200, 16, clade_size=8), ("G_off", "G_tet"))
+    T = pb["T"].copy()
+    T[3, 7] += 2
+    pb = dict(pb, T=T)
+    engine.load(**pb)
+    assert engine.load_info() == "legacy"
+    res = engine.compute(0)
+    _check_rows(engine, pb, (0, 7, 100, 198), res)
+
+
+def test_g_only_long_list_takes_the_general_sort(engine):
+    """A (genome, protein) list of 9 000 tetramers does not fit the record's
+    13-bit list offset: F is built by the general radix sort and the fused
+    row kernel takes the long list; results equal the F + G load."""
+    rng = np.random.default_rng(5)
+    n, P = 30, 3
+    sets = {(g, p): np.unique(rng.integers(0, 4000, 60)) for g in range(n) for p in range(P)}
+    sets[(4, 1)] = np.arange(0, 18000, 2)
+    from helpers import sets_problem
+    pb = sets_problem({k: v.tolist() for k, v in sets.items()}, n, P)
+    engine.load(**pb)
+    ref = engine.compute(0)
+    engine.load(**_strip(pb, ("Lp", "F_prot", "F_genome")))
+    assert engine.load_info() == "legacy"
+    got = engine.compute(0)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    _check_rows(engine, pb, (0, 4, 20), ref)

@@ -38,6 +38,8 @@ def _strip(pb, drop):
 def test_f_only_and_g_only_equal_f_plus_g(engine, compat):
     for name, pb in _problems():
         engine.load(**pb)
+        # both given: the transposition sort proves G against F (QT: G of both DBs, checked by search)
+        assert engine.load_info() == ("as_given" if name == "qt" else "g_checked"), name
         ref = engine.compute(compat)
         st = engine.stats()
         assert st["rows_kernel"] == "pl", name
@@ -48,6 +50,10 @@ def test_f_only_and_g_only_equal_f_plus_g(engine, compat):
             if name == "qt" and drop[0] == "Lp":
                 continue  # QT G of both DBs != the joined F (covered below)
             engine.load(**_strip(pb, drop))
+            # F only: G by the sort, list bounds from T (QT's T counts both DBs' full lists, not the
+            # joined F: the general radix sort); G only: F by the sort
+            want = "f_from_g" if drop[0] == "Lp" else ("legacy" if name == "qt" else "g_from_f")
+            assert engine.load_info() == want, (name, drop)
             got = engine.compute(compat)
             st2 = engine.stats()
             assert st2["rows_kernel"] == "pl", (name, drop)

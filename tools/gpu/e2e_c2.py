@@ -8,7 +8,8 @@ SCPs): the same SQLite DB through
            no E, ParFAAIHipImpl on the GPU) -- if built,
   ref      oracle/_ref/par_fastaai.x (the reference, built from its sources),
 each run --repeats times (medians reported), the reference with
-OMP_NUM_THREADS = this process's usable CPUs (BASELINE.md plan) unless
+OMP_NUM_THREADS = this process's usable CPUs (affinity capped by the cgroup quota,
+bench.usable_cpus; BASELINE.md plan) unless
 --threads is given; all CSV outputs must be byte identical.  Prints one JSON
 line with the walls, every run's phase lines and the host.
 
