@@ -471,7 +471,7 @@ int ensure_scan(pfaai_ctx* c, int64_t n) {
 }
 
 template <int DB, class S0, class DN>
-void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int passes, hipStream_t s) {
+void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, int passes, hipStream_t s) {
     const int64_t ntiles = ceil_div(n, kSortTile), ngroups = ceil_div(ntiles, kSortGroup);
     auto* hist = static_cast<uint32_t*>(c->shist.p);
     auto* gsum = static_cast<uint32_t*>(c->sgsum.p);
@@ -481,18 +481,21 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int p
     for (int pass = 0; pass < passes; ++pass) {
         const int shift = pass * DB;
         const bool last = pass == passes - 1;
+        // the digit covers only key bits: the records carry other fields right above the key
+        const uint32_t mask = (1u << std::min(DB, kb - shift)) - 1u;
         const SrcRecs prev{buf[(pass + 1) & 1]};  // pass p reads what pass p - 1 wrote
         const DstRecs next{buf[pass & 1]};
         if (pass == 0)
-            hipLaunchKernelGGL((k_sort_hist<DB, S0>), dim3(ntiles), dim3(kSortThreads), 0, s, src0, n, shift, hist);
+            hipLaunchKernelGGL((k_sort_hist<DB, S0>), dim3(ntiles), dim3(kSortThreads), 0, s, src0, n, shift, mask,
+                               hist);
         else
             hipLaunchKernelGGL((k_sort_hist<DB, SrcRecs>), dim3(ntiles), dim3(kSortThreads), 0, s, prev, n, shift,
-                               hist);
+                               mask, hist);
         hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
         hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base);
 #define SC(SRC_T, SRC, DST_T, DST)                                                                        \
     hipLaunchKernelGGL((k_sort_scatter<DB, SRC_T, DST_T>), dim3(ntiles), dim3(kSortThreads), lds, s, SRC, DST, n, \
-                       shift, hist, gsum, base)
+                       shift, mask, hist, gsum, base)
         if (pass == 0 && last) SC(S0, src0, DN, dstN);
         else if (pass == 0) SC(S0, src0, DstRecs, next);
         else if (last) SC(SrcRecs, prev, DN, dstN);
@@ -508,10 +511,10 @@ int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipSt
     if (n == 0) return PFAAI_RC_OK;
     int passes;
     switch (tsort_db(kb, &passes)) {
-        case 8: tsort_launch<8>(c, src0, dstN, n, passes, s); break;
-        case 9: tsort_launch<9>(c, src0, dstN, n, passes, s); break;
-        case 10: tsort_launch<10>(c, src0, dstN, n, passes, s); break;
-        default: tsort_launch<11>(c, src0, dstN, n, passes, s); break;
+        case 8: tsort_launch<8>(c, src0, dstN, n, kb, passes, s); break;
+        case 9: tsort_launch<9>(c, src0, dstN, n, kb, passes, s); break;
+        case 10: tsort_launch<10>(c, src0, dstN, n, kb, passes, s); break;
+        default: tsort_launch<11>(c, src0, dstN, n, kb, passes, s); break;
     }
     HIPCHK(c, hipGetLastError());
     return PFAAI_RC_OK;

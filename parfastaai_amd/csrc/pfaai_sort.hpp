@@ -143,7 +143,7 @@ struct DstFFromG {
 // ---- the pass kernels -------------------------------------------------------
 
 template <int DB, class Src>
-__global__ __launch_bounds__(kSortThreads) void k_sort_hist(Src src, int64_t n, int shift,
+__global__ __launch_bounds__(kSortThreads) void k_sort_hist(Src src, int64_t n, int shift, uint32_t mask,
                                                             uint32_t* __restrict__ hist) {
     constexpr int BINS = 1 << DB;
     __shared__ uint32_t h[BINS];
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_hist(Src src, int64_t n, 
 #pragma unroll
     for (int k = 0; k < kSortItems; ++k) {  // every load issued before the first LDS atomic
         const int64_t i = t0 + k * kSortThreads + threadIdx.x;
-        d[k] = i < n ? sort_digit(src.hist_rec(i), shift, BINS - 1) : 0xFFFFFFFFu;
+        d[k] = i < n ? sort_digit(src.hist_rec(i), shift, mask) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; ++k)
@@ -257,12 +257,12 @@ constexpr size_t sort_scatter_lds() {
 }
 
 template <int DB, class Src, class Dst>
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst, int64_t n, int shift,
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst, int64_t n, int shift, uint32_t mask,
                                                                const uint32_t* __restrict__ hist,
                                                                const uint32_t* __restrict__ gsum,
                                                                const uint32_t* __restrict__ binbase) {
     constexpr int BINS = 1 << DB, W = kSortThreads / 64;
-    constexpr uint32_t MASK = BINS - 1;
+    const uint32_t MASK = mask;  // the digit's bits of the key only: record fields follow the key directly
     extern __shared__ __align__(16) unsigned char sort_lds[];
     uint64_t* srt = reinterpret_cast<uint64_t*>(sort_lds);                              // [kSortTile]
     uint32_t* lstart = reinterpret_cast<uint32_t*>(sort_lds + (size_t)kSortTile * 8);  // [BINS]
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
         const uint32_t d = sort_digit(rec[k], shift, MASK);
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int bit = 0; bit < DB; ++bit) {
+        for (int bit = 0; bit < DB; ++bit) {  // (bits above the mask are 0 in every lane: same ballot)
             const bool on = (d >> bit) & 1u;
             const uint64_t m = __ballot(on);
             peers &= on ? m : ~m;
