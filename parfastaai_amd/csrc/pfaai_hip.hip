@@ -478,6 +478,11 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
     auto* base = static_cast<uint32_t*>(c->sbase.p);
     uint64_t* buf[2] = {static_cast<uint64_t*>(c->srec_a.p), static_cast<uint64_t*>(c->srec_b.p)};
     const size_t lds = sort_scatter_lds<DB>();
+    // persistent scatter: one 1024-thread workgroup per CU (its LDS tile and
+    // counters take ~104 KB of the 160), each walking ntiles / grid tiles
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int grid = (int)std::min<int64_t>(ntiles, cus);
     for (int pass = 0; pass < passes; ++pass) {
         const int shift = pass * DB;
         const bool last = pass == passes - 1;
@@ -494,8 +499,8 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
         hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
         hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base);
 #define SC(SRC_T, SRC, DST_T, DST)                                                                        \
-    hipLaunchKernelGGL((k_sort_scatter<DB, SRC_T, DST_T>), dim3(ntiles), dim3(kSortThreads), lds, s, SRC, DST, n, \
-                       shift, mask, hist, gsum, base)
+    hipLaunchKernelGGL((k_sort_scatter<DB, SRC_T, DST_T>), dim3(grid), dim3(kSortThreads), lds, s, SRC, DST, n, \
+                       ntiles, shift, mask, hist, gsum, base)
         if (pass == 0 && last) SC(S0, src0, DN, dstN);
         else if (pass == 0) SC(S0, src0, DstRecs, next);
         else if (last) SC(SrcRecs, prev, DN, dstN);
@@ -537,10 +542,15 @@ int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipS
     HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
-    const DstGposCheck dst{want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr,
-                           static_cast<const int32_t*>(c->G_tet.p), static_cast<const int64_t*>(c->G_off.p),
-                           static_cast<const int64_t*>(c->Lp.p), err};
+    // G_pos is the sort's output even when the row kernels will not use it: the
+    // tetramer check reads it (srec_b's space when G_pos is not kept)
+    if (!want_pos && (rc = ensure(c, c->srec_b, n_f * 4))) return rc;
+    auto* gpos = static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->srec_b.p);
+    const DstGposCheck dst{gpos, static_cast<const int64_t*>(c->G_off.p), err};
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
+    hipLaunchKernelGGL(k_check_gpos, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 8192)), dim3(256), 0, s,
+                       static_cast<const int32_t*>(c->G_tet.p), gpos, static_cast<const int64_t*>(c->Lp.p), n_f, err);
+    HIPCHK(c, hipGetLastError());
     int bad = 0;
     HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));

@@ -70,31 +70,37 @@ struct SrcRecs {
 };
 
 // ---- destinations (last pass) ----------------------------------------------
+// The write phase is split so that a tile's dependent loads are issued
+// together: fetch(pos, v) loads what store needs (Aux), then store(pos, v,
+// aux) writes -- eight records per thread, every fetch before the first store.
 
 struct DstRecs {
     uint64_t* r;
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v) const { r[pos] = v; }
+    struct Aux {};
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
+    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux) const { r[pos] = v; }
 };
 
 // Both F and G given (records key g * P + p | F index << 32, sorted = F's
-// genome-major transpose): G_pos[pos] = F index, and the caller's G must BE
-// that transpose -- its tetramer at pos is the F entry's (Lp[t] <= i <
-// Lp[t + 1]) and its list (g, p) spans pos (G_off[key] <= pos < G_off[key +
-// 1]; with |G| = |F| and G_off monotone that pins every list bound).  Any
-// mismatch sets *err.
+// genome-major transpose): G_pos[pos] = F index, and the caller's list
+// bounds must span pos (G_off[key] <= pos < G_off[key + 1]: with |G| = |F|
+// and G_off monotone that pins every list bound; any mismatch sets *err).
+// That the caller's tetramer at pos is the F entry's is checked afterwards
+// by k_check_gpos, a streaming pass (not a dependent load chain here).
 struct DstGposCheck {
     uint32_t* G_pos;
-    const int32_t* G_tet;
     const int64_t* G_off;
-    const int64_t* Lp;
     int* err;
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v) const {
-        const uint32_t key = (uint32_t)v, i = (uint32_t)(v >> 32);
-        if (G_pos) G_pos[pos] = i;
-        const int32_t t = G_tet[pos];
-        const bool ok = (uint32_t)t < (uint32_t)kNTetramers && Lp[t] <= (int64_t)i && (int64_t)i < Lp[t + 1] &&
-                        G_off[key] <= pos && pos < G_off[key + 1];
-        if (!ok) atomicOr(err, 1);
+    struct Aux {
+        uint32_t lo, hi;  // list bounds (< 2^32: |G| = |F| <= 2^32 - 64)
+    };
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
+        const uint32_t key = (uint32_t)v;
+        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1]};
+    }
+    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
+        G_pos[pos] = (uint32_t)(v >> 32);
+        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
     }
 };
 
@@ -110,13 +116,18 @@ struct DstGFromF {
     const int64_t* Lp;
     int kb;
     int* err;
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v) const {
+    struct Aux {
+        uint32_t lo, hi, lp;  // (all < 2^32: |F| <= 2^32 - 64)
+    };
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
         const uint32_t key = (uint32_t)v & ((1u << kb) - 1u);
         const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
-        const int64_t i = Lp[t] + (int64_t)(v >> (kb + 18));
-        G_tet[pos] = t;
-        if (G_pos) G_pos[pos] = (uint32_t)i;
-        if (!(G_off[key] <= pos && pos < G_off[key + 1])) atomicOr(err, 1);
+        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u};
+    }
+    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
+        G_tet[pos] = (int32_t)((v >> kb) & 0x3FFFFu);
+        if (G_pos) G_pos[pos] = a.lp + (uint32_t)(v >> (kb + 18));
+        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
     }
 };
 
@@ -131,14 +142,34 @@ struct DstFFromG {
     uint32_t* G_pos;  // nullable
     const int64_t* G_off;
     uint32_t P;
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v) const {
+    struct Aux {
+        uint32_t k0;
+    };
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
+        const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
+        return {G_pos ? (uint32_t)G_off[(int64_t)g * P + p] : 0u};
+    }
+    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
         const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
         Fp[pos] = (int32_t)p;
         Fg[pos] = (int32_t)g;
         fp16[pos] = (uint16_t)p;
-        if (G_pos) G_pos[G_off[(int64_t)g * P + p] + (int64_t)(v >> 51)] = (uint32_t)pos;
+        if (G_pos) G_pos[(int64_t)a.k0 + (int64_t)(v >> 51)] = (uint32_t)pos;
     }
 };
+
+// Both given, after the sort: the caller's tetramer of every G entry k is
+// the one of F entry G_pos[k] (Lp[t] <= i < Lp[t + 1]); a streaming pass.
+__global__ void k_check_gpos(const int32_t* __restrict__ G_tet, const uint32_t* __restrict__ G_pos,
+                             const int64_t* __restrict__ Lp, int64_t n, int* __restrict__ err) {
+    bool bad = false;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t t = G_tet[k];
+        const int64_t i = G_pos[k];
+        bad |= !((uint32_t)t < (uint32_t)kNTetramers && Lp[t] <= i && i < Lp[t + 1]);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 1);
+}
 
 // ---- the pass kernels -------------------------------------------------------
 
@@ -257,75 +288,93 @@ constexpr size_t sort_scatter_lds() {
 }
 
 template <int DB, class Src, class Dst>
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst, int64_t n, int shift, uint32_t mask,
-                                                               const uint32_t* __restrict__ hist,
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst, int64_t n, int64_t ntiles, int shift,
+                                                               uint32_t mask, const uint32_t* __restrict__ hist,
                                                                const uint32_t* __restrict__ gsum,
                                                                const uint32_t* __restrict__ binbase) {
     constexpr int BINS = 1 << DB, W = kSortThreads / 64;
-    const uint32_t MASK = mask;  // the digit's bits of the key only: record fields follow the key directly
+    constexpr int BPT = BINS > kSortThreads ? BINS / kSortThreads : 1;  // digits per thread (scans)
     extern __shared__ __align__(16) unsigned char sort_lds[];
     uint64_t* srt = reinterpret_cast<uint64_t*>(sort_lds);                              // [kSortTile]
     uint32_t* lstart = reinterpret_cast<uint32_t*>(sort_lds + (size_t)kSortTile * 8);  // [BINS]
     uint32_t* gbase = lstart + BINS;                                                    // [BINS]
     uint16_t* cnt = reinterpret_cast<uint16_t*>(gbase + BINS);                          // [W][BINS]
+    __shared__ uint32_t wsum[W];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t tile = blockIdx.x, t0 = tile * kSortTile, grp = tile / kSortGroup;
-    // this tile's records: wave w owns [w * 512, (w + 1) * 512) of the tile,
-    // round k of it at lanes 0..63 -- rank order = (wave, round, lane) =
-    // input order, so the sort is stable
-    uint64_t rec[kSortItems];
-#pragma unroll
-    for (int k = 0; k < kSortItems; ++k) {
-        const int64_t i = t0 + (wid * kSortItems + k) * 64 + lane;
-        rec[k] = i < n ? src.load(i) : 0ull;
-    }
-    for (int b = tid; b < BINS; b += kSortThreads) {
-        gbase[b] = binbase[b] + gsum[grp * BINS + b] + hist[tile * BINS + b];
-#pragma unroll
-        for (int w = 0; w < W; ++w) cnt[w * BINS + b] = 0;
-    }
-    __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint16_t lr[kSortItems];
     uint16_t* wc = cnt + wid * BINS;
+    // a tile's records: wave w owns [w * 512, (w + 1) * 512) of it, round k
+    // at lanes 0..63 -- rank order = (wave, round, lane) = input order, so
+    // the sort is stable.  Persistent: each workgroup walks tiles blockIdx.x
+    // + j * gridDim.x and loads tile j + 1 (records and digit bases) while it
+    // ranks and writes tile j.
+    uint64_t rec[kSortItems];
+    uint32_t gb[BPT];
+    auto fetch_tile = [&](int64_t tile, uint64_t (&r)[kSortItems], uint32_t (&g)[BPT]) {
+        const int64_t t0 = tile * kSortTile;
 #pragma unroll
-    for (int k = 0; k < kSortItems; ++k) {
-        const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n;
-        const uint32_t d = sort_digit(rec[k], shift, MASK);
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < DB; ++bit) {  // (bits above the mask are 0 in every lane: same ballot)
-            const bool on = (d >> bit) & 1u;
-            const uint64_t m = __ballot(on);
-            peers &= on ? m : ~m;
+        for (int k = 0; k < kSortItems; ++k) {
+            const int64_t i = t0 + (wid * kSortItems + k) * 64 + lane;
+            r[k] = (tile < ntiles && i < n) ? src.load(i) : 0ull;
         }
-        const uint32_t r = (uint32_t)__popcll(peers & lt), c = (uint32_t)__popcll(peers);
-        const uint32_t base = valid ? wc[d] : 0u;
-        lr[k] = (uint16_t)(base + r);
-        if (valid && r + 1 == c) wc[d] = (uint16_t)(base + c);  // the group's last lane advances the counter
-    }
-    __syncthreads();
-    // per digit: the waves' counts -> exclusive prefix over waves; the tile's total
-    for (int b = tid; b < BINS; b += kSortThreads) {
-        uint32_t run = 0;
+        const int64_t grp = tile / kSortGroup;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint32_t v = cnt[w * BINS + b];
-            cnt[w * BINS + b] = (uint16_t)run;
-            run += v;
+        for (int q = 0; q < BPT; ++q) {
+            const int b = tid + q * kSortThreads;
+            g[q] = (tile < ntiles && b < BINS) ? binbase[b] + gsum[grp * BINS + b] + hist[tile * BINS + b] : 0u;
         }
-        lstart[b] = run;
-    }
-    __syncthreads();
-    {  // exclusive scan of the digit totals over the digits (BPT consecutive digits per thread)
-        constexpr int BPT = BINS > kSortThreads ? BINS / kSortThreads : 1;
-        __shared__ uint32_t wsum[W];
-        uint32_t v[BPT], mine = 0;
+    };
+    fetch_tile(blockIdx.x, rec, gb);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kSortTile;
+        uint64_t nrec[kSortItems];
+        uint32_t ngb[BPT];
+        fetch_tile(tile + gridDim.x, nrec, ngb);  // in flight during this tile
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int b = tid + q * kSortThreads;
+            if (b < BINS) {
+                gbase[b] = gb[q];
+#pragma unroll
+                for (int w = 0; w < W; ++w) cnt[w * BINS + b] = 0;
+            }
+        }
+        __syncthreads();
+        uint16_t lr[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; ++k) {
+            const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n;
+            const uint32_t d = sort_digit(rec[k], shift, mask);
+            uint64_t peers = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < DB; ++bit) {  // (bits above the mask are 0 in every lane: same ballot)
+                const bool on = (d >> bit) & 1u;
+                const uint64_t m = __ballot(on);
+                peers &= on ? m : ~m;
+            }
+            const uint32_t r = (uint32_t)__popcll(peers & lt), c = (uint32_t)__popcll(peers);
+            const uint32_t base = valid ? wc[d] : 0u;
+            lr[k] = (uint16_t)(base + r);
+            if (valid && r + 1 == c) wc[d] = (uint16_t)(base + c);  // the group's last lane advances the counter
+        }
+        __syncthreads();
+        // per digit: the waves' counts -> exclusive prefix over waves; the
+        // tile's total, then its exclusive scan over the digits
+        uint32_t tot[BPT], mine = 0;
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
             const int b = tid * BPT + q;
-            v[q] = b < BINS ? lstart[b] : 0u;
-            mine += v[q];
+            uint32_t run = 0;
+            if (b < BINS) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t v = cnt[w * BINS + b];
+                    cnt[w * BINS + b] = (uint16_t)run;
+                    run += v;
+                }
+            }
+            tot[q] = run;
+            mine += run;
         }
         uint32_t inc = mine;
 #pragma unroll
@@ -341,23 +390,45 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
         for (int q = 0; q < BPT; ++q) {
             const int b = tid * BPT + q;
             if (b < BINS) lstart[b] = off;
-            off += v[q];
+            off += tot[q];
         }
-    }
-    __syncthreads();
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kSortItems; ++k) {
-        if (t0 + (wid * kSortItems + k) * 64 + lane < n) {
-            const uint32_t d = sort_digit(rec[k], shift, MASK);
-            srt[lstart[d] + cnt[wid * BINS + d] + lr[k]] = rec[k];
+        for (int k = 0; k < kSortItems; ++k) {
+            if (t0 + (wid * kSortItems + k) * 64 + lane < n) {
+                const uint32_t d = sort_digit(rec[k], shift, mask);
+                srt[lstart[d] + cnt[wid * BINS + d] + lr[k]] = rec[k];
+            }
         }
-    }
-    __syncthreads();
-    const int tn = (int)((n - t0) < kSortTile ? (n - t0) : kSortTile);
-    for (int lp = tid; lp < tn; lp += kSortThreads) {
-        const uint64_t v = srt[lp];
-        const uint32_t d = sort_digit(v, shift, MASK);
-        dst.store((int64_t)gbase[d] + (lp - (int)lstart[d]), v);
+        __syncthreads();
+        // write the tile in digit order: each digit's run is contiguous in the output
+        // (positions are < 2^32: n <= 2^32 - 64; records re-read from LDS for the stores)
+        const int tn = (int)((n - t0) < kSortTile ? (n - t0) : kSortTile);
+#pragma unroll
+        for (int h = 0; h < kSortItems; h += kSortItems / 2) {  // two halves: fewer live registers
+            uint32_t pos[kSortItems / 2];
+            typename Dst::Aux aux[kSortItems / 2];
+#pragma unroll
+            for (int k = 0; k < kSortItems / 2; ++k) {
+                const int lp = tid + (h + k) * kSortThreads;
+                if (lp < tn) {
+                    const uint64_t v = srt[lp];
+                    const uint32_t d = sort_digit(v, shift, mask);
+                    pos[k] = gbase[d] + (uint32_t)(lp - (int)lstart[d]);
+                    aux[k] = dst.fetch(pos[k], v);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kSortItems / 2; ++k) {
+                const int lp = tid + (h + k) * kSortThreads;
+                if (lp < tn) dst.store(pos[k], srt[lp], aux[k]);
+            }
+        }
+        __syncthreads();  // the LDS tile, counters and bases are rewritten by the next tile
+#pragma unroll
+        for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
     }
 }
 
