@@ -104,30 +104,39 @@ struct DstGposCheck {
     }
 };
 
-// F only (records key g * P + p | t << kb | j << (kb + 18), F index Lp[t] +
-// j, from k_fkeys_rec): G_tet / G_pos at the sorted position; G_off comes
-// from T (T[p][g] is the length of list (g, p) in a consistent problem) and
-// is verified like DstGposCheck's (a mismatch sets *err: the caller rebuilds
-// G the general way).
-struct DstGFromF {
-    uint32_t* G_pos;  // nullable
-    int32_t* G_tet;
+// Records key g * P + p | t << kb | j << (kb + 18) from k_fkeys_rec (F index
+// Lp[t] + j; the tetramer travels with the record), sorted = F's genome-major
+// transpose.  Writes G_pos (if kept) and either
+//   builds  G_tet (F only; G_off comes from T -- T[p][g] is the length of list
+//           (g, p) in a consistent problem -- and must span every position:
+//           a mismatch sets *err and the caller rebuilds G the general way), or
+//   checks  the caller's G (both given): its tetramer at the position must be
+//           the record's and its list (g, p) must span the position (with
+//           |G| = |F| and G_off monotone that pins every list bound); a
+//           mismatch sets *err.
+struct DstGFromRecs {
+    uint32_t* G_pos;           // nullable
+    int32_t* G_tet_out;        // build: written
+    const int32_t* G_tet_in;   // check: compared
     const int64_t* G_off;
     const int64_t* Lp;
     int kb;
     int* err;
     struct Aux {
         uint32_t lo, hi, lp;  // (all < 2^32: |F| <= 2^32 - 64)
+        int32_t tu;
     };
-    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
+    __device__ __forceinline__ Aux fetch(int64_t pos, uint64_t v) const {
         const uint32_t key = (uint32_t)v & ((1u << kb) - 1u);
         const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
-        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u};
+        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u,
+                G_tet_in ? G_tet_in[pos] : t};
     }
     __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
-        G_tet[pos] = (int32_t)((v >> kb) & 0x3FFFFu);
+        const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
+        if (G_tet_out) G_tet_out[pos] = t;
         if (G_pos) G_pos[pos] = a.lp + (uint32_t)(v >> (kb + 18));
-        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
+        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi && a.tu == t)) atomicOr(err, 1);
     }
 };
 
@@ -434,9 +443,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
 
 // ---- keygen kernels (paths whose first pass needs a materialised record) ----
 
-// F only: one workgroup per tetramer block (grid-stride): rec = key g * P + p
-// | t << kb | (i - Lp[t]) << (kb + 18), and T-derived list lengths are not
-// needed here (G_off comes from T).
+// F -> records for DstGFromRecs: one workgroup per tetramer block
+// (grid-stride), so the tetramer of every entry is known without a search:
+// rec = key g * P + p | t << kb | (i - Lp[t]) << (kb + 18); also the u16
+// protein column.
 __global__ __launch_bounds__(256) void k_fkeys_rec(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                    const int32_t* __restrict__ Fg, uint32_t P, int kb,
                                                    uint64_t* __restrict__ rec, uint16_t* __restrict__ fp16) {
