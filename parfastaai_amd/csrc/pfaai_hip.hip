@@ -480,9 +480,11 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
     const size_t lds = sort_scatter_lds<DB>();
     // persistent scatter: one 1024-thread workgroup per CU (its LDS tile and
     // counters take ~104 KB of the 160), each walking ntiles / grid tiles
-    int cus = 256;
+    int cus = 256, per_cu = 1;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    const int grid = (int)std::min<int64_t>(ntiles, cus);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_sort_scatter<DB, SrcRecs, DstRecs>),
+                                                       kSortThreads, lds);
+    const int grid = (int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per_cu));
     for (int pass = 0; pass < passes; ++pass) {
         const int shift = pass * DB;
         const bool last = pass == passes - 1;
@@ -515,7 +517,12 @@ template <class S0, class DN>
 int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipStream_t s) {
     if (n == 0) return PFAAI_RC_OK;
     int passes;
-    switch (tsort_db(kb, &passes)) {
+    int db = tsort_db(kb, &passes);
+    if (const char* v = DIAG_ENV("PFAAI_TSORT_DB")) {  // diagnostics: digit width (A/B)
+        db = std::max(8, std::min(kSortMaxDB, atoi(v)));
+        passes = (kb + db - 1) / db;
+    }
+    switch (db) {
         case 8: tsort_launch<8>(c, src0, dstN, n, kb, passes, s); break;
         case 9: tsort_launch<9>(c, src0, dstN, n, kb, passes, s); break;
         case 10: tsort_launch<10>(c, src0, dstN, n, kb, passes, s); break;
