@@ -6,6 +6,7 @@
 // F-only input, the sorted work lists, then the row kernel (K-S+J).
 
 #include <algorithm>
+#include <random>
 #include <atomic>
 #include <thread>
 #include <cstdio>
@@ -536,37 +537,33 @@ void release_tsort(pfaai_ctx* c) {
     for (DevBuf* b : {&c->srec_a, &c->srec_b, &c->shist, &c->sgsum, &c->sbase}) release(*b);
 }
 
-// F -> records (k_fkeys_rec: key, tetramer, block offset) -> the two-pass
-// sort -> DstGFromRecs.  check: the caller's G (already on the device) is
-// compared; else G_off comes from T and G_tet is written.  Returns -1 on a
-// mismatch.
-int g_from_f_records(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_pos, bool check, hipStream_t s) {
+// F only: G_off from T, records (k_fkeys_rec: key, tetramer, block offset)
+// -> the sort -> DstGFromRecs builds G_tet / G_pos.  Returns -1 if the
+// records do not fit 64 bits or T disagrees with F: the caller takes
+// build_g_from_f.
+int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_pos, hipStream_t s) {
     const int32_t P = c->prob.n_prot, ni = c->prob.n_ids;
     const int kb = bits_for(ng);
+    if (kb + 18 + jb > 64) return -1;
     int rc;
-    if ((rc = ensure_tsort(c, n_f, kb, true))) return rc;
-    if (!check && ((rc = ensure(c, c->G_off, (ng + 1) * 8)) || (rc = ensure(c, c->G_tet, std::max<int64_t>(n_f, 1) * 4)) ||
-                   (rc = ensure(c, c->cnt_t, std::max<int64_t>(ng, 1) * 4)) || (rc = ensure_scan(c, ng))))
+    if ((rc = ensure_tsort(c, n_f, kb, true)) || (rc = ensure(c, c->G_off, (ng + 1) * 8)) ||
+        (rc = ensure(c, c->G_tet, std::max<int64_t>(n_f, 1) * 4)) || (rc = ensure(c, c->cnt_t, std::max<int64_t>(ng, 1) * 4)) ||
+        (rc = ensure_scan(c, ng)))
         return rc;
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
     HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
-    if (!check) {
-        auto* len = static_cast<uint32_t*>(c->cnt_t.p);
-        hipLaunchKernelGGL(k_len_from_t, dim3((int)std::min<int64_t>(ceil_div(ng, 256), 8192)), dim3(256), 0, s,
-                           static_cast<const int32_t*>(c->T.p), P, ni, c->prob.t_cols, len);
-        if ((rc = scan_u32(c, len, ng, static_cast<unsigned long long*>(c->G_off.p), s))) return rc;
-    }
+    auto* len = static_cast<uint32_t*>(c->cnt_t.p);
+    hipLaunchKernelGGL(k_len_from_t, dim3((int)std::min<int64_t>(ceil_div(ng, 256), 8192)), dim3(256), 0, s,
+                       static_cast<const int32_t*>(c->T.p), P, ni, c->prob.t_cols, len);
+    if ((rc = scan_u32(c, len, ng, static_cast<unsigned long long*>(c->G_off.p), s))) return rc;
     hipLaunchKernelGGL(k_fkeys_rec, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
                        static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), (uint32_t)P, kb,
                        static_cast<uint64_t*>(c->srec_b.p), static_cast<uint16_t*>(c->Fp16.p));
     HIPCHK(c, hipGetLastError());
     const SrcRecs src{static_cast<const uint64_t*>(c->srec_b.p)};
-    const DstGFromRecs dst{want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr,
-                           check ? nullptr : static_cast<int32_t*>(c->G_tet.p),
-                           check ? static_cast<const int32_t*>(c->G_tet.p) : nullptr,
+    const DstGFromRecs dst{want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr, static_cast<int32_t*>(c->G_tet.p),
                            static_cast<const int64_t*>(c->G_off.p), static_cast<const int64_t*>(c->Lp.p), kb, err};
-    (void)jb;
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
     int bad = 0;
     HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -575,42 +572,38 @@ int g_from_f_records(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_po
 }
 
 // Both F and G given with |G| = |F|: G must be F's genome-major transpose.
-// One two-pass sort of F by (genome, protein) proves it against the caller's
-// lists and yields G_pos (and the u16 protein column) on the way: records
-// carrying the tetramer when key, tetramer and block offset fit 64 bits
-// (g_from_f_records), else records (key, F index) and a streaming tetramer
-// check afterwards (k_check_gpos).  Returns -1 on a mismatch.
-int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_pos, hipStream_t s) {
+// One two-pass sort of F by (genome, protein) -- records (key, F index),
+// read straight from F -- yields G_pos and checks the caller's list bounds
+// per entry and its tetramers by the keyed pair-hash sums (DstGposHash,
+// k_hash_f).  Returns -1 on a mismatch.
+int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipStream_t s) {
     const int kb = bits_for(ng);
-    if (kb + 18 + jb <= 64) return g_from_f_records(c, ng, n_f, jb, want_pos, true, s);
     int rc;
     if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
+    // G_pos is the sort's output even when the row kernels will not use it
+    // (srec_b's space then)
+    if (!want_pos && (rc = ensure(c, c->srec_b, n_f * 4))) return rc;
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
+    auto* sums = sc + SC_HG;  // [0]: over G, [1]: over F (SC_HF)
     HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
+    HIPCHK(c, hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), s));
+    const uint64_t seed = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
+                          (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
-    // G_pos is the sort's output even when the row kernels will not use it: the
-    // tetramer check reads it (srec_b's space when G_pos is not kept)
-    if (!want_pos && (rc = ensure(c, c->srec_b, n_f * 4))) return rc;
-    auto* gpos = static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->srec_b.p);
-    const DstGposCheck dst{gpos, static_cast<const int64_t*>(c->G_off.p), err};
+    const DstGposHash dst{static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->srec_b.p),
+                          static_cast<const int32_t*>(c->G_tet.p), static_cast<const int64_t*>(c->G_off.p), seed, err,
+                          sums};
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
-    hipLaunchKernelGGL(k_check_gpos, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 8192)), dim3(256), 0, s,
-                       static_cast<const int32_t*>(c->G_tet.p), gpos, static_cast<const int64_t*>(c->Lp.p), n_f, err);
+    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p), seed, sums + 1);
     HIPCHK(c, hipGetLastError());
     int bad = 0;
+    unsigned long long h[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(h, sums, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    return bad ? -1 : PFAAI_RC_OK;
-}
-
-// F only: G_off from T, then g_from_f_records builds G_tet / G_pos.
-// Returns -1 if the records do not fit 64 bits or T disagrees with F: the
-// caller takes build_g_from_f.
-int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool want_pos, hipStream_t s) {
-    if (bits_for(ng) + 18 + jb > 64) return -1;
-    return g_from_f_records(c, ng, n_f, jb, want_pos, false, s);
+    return (bad || h[0] != h[1]) ? -1 : PFAAI_RC_OK;
 }
 
 // G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
@@ -916,7 +909,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
         // the transpose of F -- one sort of F by (genome, protein) proves it
         // against the caller's lists (and yields G_pos): no search per entry
-        rc = check_g_transpose(c, ng, n_f, bits_for(max_lc + 1), want_pos, s);
+        rc = check_g_transpose(c, ng, n_f, want_pos, s);
         if (rc == -1)
             return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
         if (rc) return rc;

@@ -76,67 +76,103 @@ struct SrcRecs {
 
 struct DstRecs {
     uint64_t* r;
+    static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux) const { r[pos] = v; }
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
+        r[pos] = v;
+        return 0;
+    }
 };
 
 // Both F and G given (records key g * P + p | F index << 32, sorted = F's
-// genome-major transpose): G_pos[pos] = F index, and the caller's list
-// bounds must span pos (G_off[key] <= pos < G_off[key + 1]: with |G| = |F|
-// and G_off monotone that pins every list bound; any mismatch sets *err).
-// That the caller's tetramer at pos is the F entry's is checked afterwards
-// by k_check_gpos, a streaming pass (not a dependent load chain here).
-struct DstGposCheck {
+// genome-major transpose): G_pos[pos] = F index i, and the caller's G must BE
+// that transpose --
+//   list bounds: its list (g, p) must span pos (G_off[key] <= pos <
+//     G_off[key + 1]; with |G| = |F| and G_off monotone that pins every
+//     list bound); a mismatch sets *err;
+//   tetramers: its tetramer at pos must be F entry i's.  F entry i's tetramer
+//     is not in the record (key 21 + tetramer 18 + index 30 bits do not fit
+//     64), so the check is a keyed hash of the pairs: the sum over G of
+//     h(G_pos[k], G_tet[k]) (here, from coalesced reads) must equal the sum
+//     over F of h(i, t(i)) (k_hash_f, from Lp alone).  G_pos is a bijection
+//     onto F by construction, so the sums differ unless every tetramer
+//     matches, except with probability ~2^-64 (h is a 64-bit mix of the
+//     injective (i, t) code, keyed by a per-load random seed).
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser (a bijection)
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ uint64_t pair_hash(uint64_t seed, uint64_t i, uint32_t t) {
+    return mix64(seed ^ ((i << 18) | t));  // i < 2^32, t < 2^18: an injective 50-bit code
+}
+
+struct DstGposHash {
     uint32_t* G_pos;
+    const int32_t* G_tet;
     const int64_t* G_off;
+    uint64_t seed;
     int* err;
+    unsigned long long* sum;
+    static constexpr bool kSum = true;
     struct Aux {
         uint32_t lo, hi;  // list bounds (< 2^32: |G| = |F| <= 2^32 - 64)
+        int32_t tu;
     };
-    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
+    __device__ __forceinline__ Aux fetch(int64_t pos, uint64_t v) const {
         const uint32_t key = (uint32_t)v;
-        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1]};
+        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_tet[pos]};
     }
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
-        G_pos[pos] = (uint32_t)(v >> 32);
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
+        const uint32_t i = (uint32_t)(v >> 32);
+        G_pos[pos] = i;
         if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
+        return pair_hash(seed, i, (uint32_t)a.tu & 0x3FFFFu) + (uint64_t)((uint32_t)a.tu >> 18);  // (t >= 2^18: never equal)
     }
 };
 
-// Records key g * P + p | t << kb | j << (kb + 18) from k_fkeys_rec (F index
-// Lp[t] + j; the tetramer travels with the record), sorted = F's genome-major
-// transpose.  Writes G_pos (if kept) and either
-//   builds  G_tet (F only; G_off comes from T -- T[p][g] is the length of list
-//           (g, p) in a consistent problem -- and must span every position:
-//           a mismatch sets *err and the caller rebuilds G the general way), or
-//   checks  the caller's G (both given): its tetramer at the position must be
-//           the record's and its list (g, p) must span the position (with
-//           |G| = |F| and G_off monotone that pins every list bound); a
-//           mismatch sets *err.
+// the F side of DstGposHash's sum: h(i, t) over every F entry i of every
+// tetramer block t -- from Lp alone, no F read
+__global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, uint64_t seed,
+                                                unsigned long long* __restrict__ sum) {
+    uint64_t acc = 0;
+    for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
+        const int64_t e = Lp[t + 1];
+        for (int64_t i = Lp[t] + threadIdx.x; i < e; i += blockDim.x) acc += pair_hash(seed, (uint64_t)i, (uint32_t)t);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sum, (unsigned long long)acc);
+}
+
+// F only (records key g * P + p | t << kb | j << (kb + 18) from k_fkeys_rec,
+// F index Lp[t] + j; the tetramer travels with the record): G_tet and G_pos
+// (if kept) at the sorted position.  G_off comes from T (T[p][g] is the
+// length of list (g, p) in a consistent problem) and must span every
+// position: a mismatch sets *err and the caller rebuilds G the general way.
 struct DstGFromRecs {
-    uint32_t* G_pos;           // nullable
-    int32_t* G_tet_out;        // build: written
-    const int32_t* G_tet_in;   // check: compared
+    uint32_t* G_pos;  // nullable
+    int32_t* G_tet;
     const int64_t* G_off;
     const int64_t* Lp;
     int kb;
     int* err;
+    static constexpr bool kSum = false;
     struct Aux {
         uint32_t lo, hi, lp;  // (all < 2^32: |F| <= 2^32 - 64)
-        int32_t tu;
     };
-    __device__ __forceinline__ Aux fetch(int64_t pos, uint64_t v) const {
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
         const uint32_t key = (uint32_t)v & ((1u << kb) - 1u);
         const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
-        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u,
-                G_tet_in ? G_tet_in[pos] : t};
+        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u};
     }
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
-        const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
-        if (G_tet_out) G_tet_out[pos] = t;
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
+        G_tet[pos] = (int32_t)((v >> kb) & 0x3FFFFu);
         if (G_pos) G_pos[pos] = a.lp + (uint32_t)(v >> (kb + 18));
-        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi && a.tu == t)) atomicOr(err, 1);
+        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
+        return 0;
     }
 };
 
@@ -151,6 +187,7 @@ struct DstFFromG {
     uint32_t* G_pos;  // nullable
     const int64_t* G_off;
     uint32_t P;
+    static constexpr bool kSum = false;
     struct Aux {
         uint32_t k0;
     };
@@ -158,27 +195,16 @@ struct DstFFromG {
         const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
         return {G_pos ? (uint32_t)G_off[(int64_t)g * P + p] : 0u};
     }
-    __device__ __forceinline__ void store(int64_t pos, uint64_t v, Aux a) const {
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
         const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
         Fp[pos] = (int32_t)p;
         Fg[pos] = (int32_t)g;
         fp16[pos] = (uint16_t)p;
         if (G_pos) G_pos[(int64_t)a.k0 + (int64_t)(v >> 51)] = (uint32_t)pos;
+        return 0;
     }
 };
 
-// Both given, after the sort: the caller's tetramer of every G entry k is
-// the one of F entry G_pos[k] (Lp[t] <= i < Lp[t + 1]); a streaming pass.
-__global__ void k_check_gpos(const int32_t* __restrict__ G_tet, const uint32_t* __restrict__ G_pos,
-                             const int64_t* __restrict__ Lp, int64_t n, int* __restrict__ err) {
-    bool bad = false;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t t = G_tet[k];
-        const int64_t i = G_pos[k];
-        bad |= !((uint32_t)t < (uint32_t)kNTetramers && Lp[t] <= i && i < Lp[t + 1]);
-    }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 1);
-}
 
 // ---- the pass kernels -------------------------------------------------------
 
@@ -333,6 +359,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
             g[q] = (tile < ntiles && b < BINS) ? binbase[b] + gsum[grp * BINS + b] + hist[tile * BINS + b] : 0u;
         }
     };
+    uint64_t hsum = 0;  // Dst::kSum: the destination's per-record sum (DstGposHash)
     fetch_tile(blockIdx.x, rec, gb);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * kSortTile;
@@ -430,7 +457,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
 #pragma unroll
             for (int k = 0; k < kSortItems / 2; ++k) {
                 const int lp = tid + (h + k) * kSortThreads;
-                if (lp < tn) dst.store(pos[k], srt[lp], aux[k]);
+                if (lp < tn) hsum += dst.store(pos[k], srt[lp], aux[k]);
             }
         }
         __syncthreads();  // the LDS tile, counters and bases are rewritten by the next tile
@@ -438,6 +465,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
         for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
 #pragma unroll
         for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
+    }
+    if constexpr (Dst::kSum) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) hsum += __shfl_down(hsum, o, 64);
+        if (lane == 0 && hsum) atomicAdd(dst.sum, (unsigned long long)hsum);
     }
 }
 

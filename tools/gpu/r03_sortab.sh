@@ -15,6 +15,8 @@ for r in list(csv.DictReader(open(f)))[:12]:
     print(f"   {float(r['TotalDurationNs'])/1e6:8.3f} ms {int(r['Calls']):3d}x avg {float(r['AverageNs'])/1e6:7.3f}  {r['Name'][:95]}")
 PY
 }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_load_sort.py tests/test_gpu_orientations.py tests/test_gpu_load_errors.py -x -q --timeout 300 --timeout-method thread > gpurun_out/sortab/pytest.log 2>&1 || { tail -30 gpurun_out/sortab/pytest.log; exit 1; }
+tail -2 gpurun_out/sortab/pytest.log
 for orient in both g; do
   for db in 8 9 10 11; do
     tag=${orient}_db$db
