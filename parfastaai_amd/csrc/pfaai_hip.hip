@@ -447,6 +447,11 @@ void release_sort_space(pfaai_ctx* c) {
 // passes and digit width for kb-bit keys: one pass up to 11 bits, two up to
 // 22 (10-bit digits for the 20-bit keys g * P + p at 10k x 100), three above
 int tsort_db(int kb, int* passes) {
+    if (const char* v = DIAG_ENV("PFAAI_TSORT_DB")) {  // diagnostics: digit width (A/B)
+        const int db = std::max(8, std::min(kSortMaxDB, atoi(v)));
+        *passes = (kb + db - 1) / db;
+        return db;
+    }
     *passes = kb <= kSortMaxDB ? 1 : kb <= 2 * kSortMaxDB ? 2 : 3;
     return std::max(8, (kb + *passes - 1) / *passes);
 }
@@ -518,11 +523,13 @@ template <class S0, class DN>
 int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipStream_t s) {
     if (n == 0) return PFAAI_RC_OK;
     int passes;
-    int db = tsort_db(kb, &passes);
-    if (const char* v = DIAG_ENV("PFAAI_TSORT_DB")) {  // diagnostics: digit width (A/B)
-        db = std::max(8, std::min(kSortMaxDB, atoi(v)));
-        passes = (kb + db - 1) / db;
-    }
+    const int db = tsort_db(kb, &passes);
+    // the ping-pong buffers this pass count writes (ensure_tsort sized them
+    // from the same tsort_db): pass p writes srec[p & 1] except the last
+    const size_t need = (size_t)n * 8;
+    if (c->srec_a.bytes < need || c->shist.bytes < (size_t)ceil_div(n, kSortTile) * (4u << db) ||
+        (passes > 2 && c->srec_b.bytes < need))
+        return fail(c, PFAAI_RC_INVALID, "internal: transposition sort buffers not sized for this pass count");
     switch (db) {
         case 8: tsort_launch<8>(c, src0, dstN, n, kb, passes, s); break;
         case 9: tsort_launch<9>(c, src0, dstN, n, kb, passes, s); break;
@@ -581,8 +588,8 @@ int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipS
     int rc;
     if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
     // G_pos is the sort's output even when the row kernels will not use it
-    // (srec_b's space then)
-    if (!want_pos && (rc = ensure(c, c->srec_b, n_f * 4))) return rc;
+    // (a scratch buffer then)
+    if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;  // (released with the sort space)
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     int* err = reinterpret_cast<int*>(sc + SC_ERR);
     auto* sums = sc + SC_HG;  // [0]: over G, [1]: over F (SC_HF)
@@ -592,7 +599,7 @@ int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipS
                           (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
-    const DstGposHash dst{static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->srec_b.p),
+    const DstGposHash dst{static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->rec_c.p),
                           static_cast<const int32_t*>(c->G_tet.p), static_cast<const int64_t*>(c->G_off.p), seed, err,
                           sums};
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
