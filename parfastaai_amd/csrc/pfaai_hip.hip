@@ -614,11 +614,11 @@ int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipS
 }
 
 // G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
-// protein-major (k_gkeys_pm; Lc counted on the way), one two-pass sort by
-// tetramer (18-bit keys, 9-bit digits) -> F (t, p, g), Fp16 and G_pos
-// (DstFFromG).  Needs P < 4096, n_ids < 2^21, lists < 8192 entries (the
-// record fields); else the caller takes build_f_from_g.
-int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, bool want_pos, hipStream_t s) {
+// protein-major (k_gkeys_pm), one two-pass sort by tetramer (18-bit keys,
+// 9-bit digits) -> F (t, p, g) and Fp16 (DstFFromG), Lp from the sorted
+// tetramers (k_rowptr).  Needs P < 4096 and n_ids < 2^21 (the record
+// fields); else the caller takes build_f_from_g.  Builds no G_pos.
+int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
     const int32_t P = c->prob.n_prot, ni = c->prob.n_ids;
     int rc;
     if ((rc = ensure_tsort(c, n, 18, true)) || (rc = ensure(c, c->cnt_t, std::max<int64_t>(n_lists, PFAAI_NTETRAMERS) * 4)) ||
@@ -629,19 +629,28 @@ int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, bool want_po
     hipLaunchKernelGGL(k_len_pm, dim3((int)std::min<int64_t>(ceil_div(n_lists, 256), 8192)), dim3(256), 0, s,
                        static_cast<const int64_t*>(c->G_off.p), P, ni, len);
     if ((rc = scan_u32(c, len, n_lists, pm_off, s))) return rc;
-    auto* lc = len;  // the lengths are consumed by the scan (stream order): reuse the buffer for Lc
-    HIPCHK(c, hipMemsetAsync(lc, 0, PFAAI_NTETRAMERS * 4, s));
     const int grid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n_lists, 4), 1), 1 << 16);
     hipLaunchKernelGGL(k_gkeys_pm, dim3(grid), dim3(256), 0, s, static_cast<const int64_t*>(c->G_off.p),
                        static_cast<const int32_t*>(c->G_tet.p), n_lists, P, ni, pm_off,
-                       static_cast<uint64_t*>(c->srec_b.p), lc);
+                       static_cast<uint64_t*>(c->srec_b.p));
     HIPCHK(c, hipGetLastError());
-    if ((rc = scan_u32(c, lc, PFAAI_NTETRAMERS, static_cast<unsigned long long*>(c->Lp.p), s))) return rc;
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(c->Lp.p, 0, (PFAAI_NTETRAMERS + 1) * 8, s));
+        return PFAAI_RC_OK;
+    }
+    // the last pass reads srec_a (two passes) or srec_b (three, diagnostics):
+    // the tetramer column goes to the one it does not read
+    int passes;
+    (void)tsort_db(18, &passes);
+    auto* ft = static_cast<uint32_t*>(passes == 2 ? c->srec_b.p : c->srec_a.p);
     const SrcRecs src{static_cast<const uint64_t*>(c->srec_b.p)};
     const DstFFromG dst{static_cast<int32_t*>(c->Fp.p), static_cast<int32_t*>(c->Fg.p),
-                        static_cast<uint16_t*>(c->Fp16.p), want_pos ? static_cast<uint32_t*>(c->G_pos.p) : nullptr,
-                        static_cast<const int64_t*>(c->G_off.p), (uint32_t)P};
-    return tsort(c, src, dst, n, 18, s);
+                        static_cast<uint16_t*>(c->Fp16.p), ft};
+    if ((rc = tsort(c, src, dst, n, 18, s))) return rc;
+    hipLaunchKernelGGL(k_rowptr, dim3(ceil_div(n, 256)), dim3(256), 0, s, ft, n, (int64_t)PFAAI_NTETRAMERS,
+                       static_cast<unsigned long long*>(c->Lp.p));
+    HIPCHK(c, hipGetLastError());
+    return PFAAI_RC_OK;
 }
 
 int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
@@ -900,17 +909,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     HIPCHK(c, hipEventRecord(c->load_ev[0], s));
     bool fp16_done = false;
     c->load_path = PFAAI_LOAD_AS_GIVEN;
-    if (!in_f) {  // G only: F (and G_pos) by the transposition sort (record fields permitting)
-        if (P < kMaxRuns && ni < (1 << 21) && c->max_glen < 8192) {
-            if ((rc = build_f_from_g_sorted(c, ng, n_f, want_pos, s))) return rc;
+    if (!in_f) {  // G only: F by the transposition sort (record fields permitting)
+        if (P < kMaxRuns && ni < (1 << 21)) {
+            if ((rc = build_f_from_g_sorted(c, ng, n_f, s))) return rc;
             fp16_done = true;
             c->load_path = PFAAI_LOAD_F_FROM_G;
         } else {
             if ((rc = build_f_from_g(c, ng, n_f, s))) return rc;
             c->load_path = PFAAI_LOAD_LEGACY;
+            pos_ok = true;  // (the general sort writes G_pos on the way)
         }
     }
-    pos_ok = !in_f;
     bool has_g = in_g;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE

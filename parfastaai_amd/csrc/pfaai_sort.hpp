@@ -176,35 +176,31 @@ struct DstGFromRecs {
     }
 };
 
-// G only (records t | p << 18 | g << 30 | j << 51 from k_gkeys_pm, enumerated
+// G only (records t | p << 18 | g << 30 from k_gkeys_pm, enumerated
 // protein-major so that the stable sort by t alone yields F's (t, p, g)
 // order): the F columns at the sorted position, the u16 protein column, and
-// G_pos of the G entry G_off[g * P + p] + j.
+// the tetramer of every position (Ft, for Lp by k_rowptr -- counting Lc by
+// atomics while generating the records cost 11 ms at 10k: 2.9e8 global
+// atomics on 160 000 counters).  No G_pos here: the inverse permutation would
+// be 2.9e8 random 4-B stores (8-14 ms at 10k) for a ~5 % faster row kernel,
+// which only repeated runs amortise (see pfaai_load).
 struct DstFFromG {
     int32_t* Fp;
     int32_t* Fg;
     uint16_t* fp16;
-    uint32_t* G_pos;  // nullable
-    const int64_t* G_off;
-    uint32_t P;
+    uint32_t* Ft;
     static constexpr bool kSum = false;
-    struct Aux {
-        uint32_t k0;
-    };
-    __device__ __forceinline__ Aux fetch(int64_t, uint64_t v) const {
-        const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
-        return {G_pos ? (uint32_t)G_off[(int64_t)g * P + p] : 0u};
-    }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
+    struct Aux {};
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
         const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
         Fp[pos] = (int32_t)p;
         Fg[pos] = (int32_t)g;
         fp16[pos] = (uint16_t)p;
-        if (G_pos) G_pos[(int64_t)a.k0 + (int64_t)(v >> 51)] = (uint32_t)pos;
+        Ft[pos] = (uint32_t)v & 0x3FFFFu;
         return 0;
     }
 };
-
 
 // ---- the pass kernels -------------------------------------------------------
 
@@ -495,22 +491,19 @@ __global__ __launch_bounds__(256) void k_fkeys_rec(const int64_t* __restrict__ L
 
 // G only: one wave per (genome, protein) list; the list's entries go to the
 // protein-major position pm_off[p * n_ids + g] + j as rec = t | p << 18 |
-// g << 30 | j << 51, and Lc[t] is counted.
+// g << 30.
 __global__ __launch_bounds__(256) void k_gkeys_pm(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
                                                   int64_t n_lists, int32_t P, int32_t n_ids,
                                                   const unsigned long long* __restrict__ pm_off,
-                                                  uint64_t* __restrict__ rec, uint32_t* __restrict__ lc) {
+                                                  uint64_t* __restrict__ rec) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t L = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); L < n_lists; L += waves) {
         const uint32_t g = (uint32_t)(L / P), p = (uint32_t)(L % P);
         const int64_t b = G_off[L], e = G_off[L + 1];
         const int64_t o = (int64_t)pm_off[(int64_t)p * n_ids + g];
-        for (int64_t k = b + lane; k < e; k += 64) {
-            const uint32_t t = (uint32_t)G_tet[k];
-            rec[o + (k - b)] = (uint64_t)t | ((uint64_t)p << 18) | ((uint64_t)g << 30) | ((uint64_t)(k - b) << 51);
-            atomicAdd(&lc[t], 1u);
-        }
+        const uint64_t pg = ((uint64_t)p << 18) | ((uint64_t)g << 30);
+        for (int64_t k = b + lane; k < e; k += 64) rec[o + (k - b)] = (uint64_t)(uint32_t)G_tet[k] | pg;
     }
 }
 

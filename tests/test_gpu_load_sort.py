@@ -9,8 +9,8 @@ two or three passes of <= 11-bit digits.
   * F only: G_off from T, verified against the sorted keys; an inconsistent
     T (a count that is not the list length) falls back to the general radix
     sort, and the results still follow the reference's formula with that T;
-  * G only: F by the protein-major enumeration sorted by tetramer; a list
-    too long for the record fields falls back to the general sort;
+  * G only: F by the protein-major enumeration sorted by tetramer (no
+    G_pos: Lp from the sorted tetramers), long lists included;
   * key widths that take one, two and three passes, and record counts that
     are not a multiple of the 8192-record tile -- bit-exact against the
     oracle and against each other.
@@ -101,10 +101,11 @@ def test_f_only_inconsistent_t_takes_the_general_sort(engine):
     _check_rows(engine, pb, (0, 7, 100, 198), res)
 
 
-def test_g_only_long_list_takes_the_general_sort(engine):
-    """A (genome, protein) list of 9 000 tetramers does not fit the record's
-    13-bit list offset: F is built by the general radix sort and the fused
-    row kernel takes the long list; results equal the F + G load."""
+def test_g_only_long_list(engine):
+    """A (genome, protein) list of 9 000 tetramers: the G-only sort's records
+    (tetramer | protein | genome) carry no list offset, so it still takes the
+    transposition sort; the fused row kernel takes the long list; results
+    equal the F + G load and the oracle."""
     rng = np.random.default_rng(5)
     n, P = 30, 3
     sets = {(g, p): np.unique(rng.integers(0, 4000, 60)) for g in range(n) for p in range(P)}
@@ -114,8 +115,9 @@ def test_g_only_long_list_takes_the_general_sort(engine):
     engine.load(**pb)
     ref = engine.compute(0)
     engine.load(**_strip(pb, ("Lp", "F_prot", "F_genome")))
-    assert engine.load_info() == "legacy"
+    assert engine.load_info() == "f_from_g"
     got = engine.compute(0)
+    assert engine.stats()["rows_kernel"] == "fused"
     for a, b in zip(got, ref):
         assert np.array_equal(a, b)
     _check_rows(engine, pb, (0, 4, 20), ref)
