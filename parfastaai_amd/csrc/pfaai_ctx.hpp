@@ -65,6 +65,7 @@ struct pfaai_ctx {
     int64_t max_glen = 0;  // longest (genome, protein) G list
     DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, G_pos, blk;
+    DevBuf G_end;  // end of the F run of every G entry (with G_pos; k_rows_pl WK 3)
     bool has_g = false;
     bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
     bool runs_key = false;

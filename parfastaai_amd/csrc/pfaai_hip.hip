@@ -341,7 +341,11 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     } else if (wl) {
         rc = build_records<MODE>(c, rb, re, s, compat);
     }
-    if (!wl && !keep) {
+    if (!wl && ends && c->dev.G_end) {
+        // WK 3 reads G_end (built at load): no run table; only the ref-compat
+        // zero-overlap quirk's first E triple
+        if (compat) rc = launch_first_key(c, s);
+    } else if (!wl && !keep) {
         rc = build_runs_g<MODE>(c, s, compat, ends);
         c->runs_valid = rc == PFAAI_RC_OK;
         c->runs_key = compat;
@@ -986,7 +990,6 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         hipLaunchKernelGGL(k_fp16, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 1 << 16)), dim3(256), 0, s,
                            static_cast<const int32_t*>(c->Fp.p), n_f, static_cast<uint16_t*>(c->Fp16.p));
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->load_ev[1], s));
     if (has_g && (rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
 
     Dev& d = c->dev;
@@ -1015,6 +1018,25 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     d.Fp16 = static_cast<const uint16_t*>(c->Fp16.p);
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
     d.T16c = c->T16c.p ? static_cast<const uint16_t*>(c->T16c.p) : d.T16;
+    // G_end with G_pos: the end of the F run of every G entry, from the
+    // run-end table looked up once here (k_blk_end + k_gend).  The WK 3 row
+    // kernel then reads (G_pos, G_end) of its G entries with coalesced loads
+    // instead of one run-table lookup per entry and step, and its steps build
+    // no run table.
+    d.G_end = nullptr;
+    c->runs_valid = false;
+    if (d.G_pos) {
+        if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
+        if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
+        hipLaunchKernelGGL(k_gend, dim3((int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, 4), 1), 1 << 16)), dim3(256),
+                           0, s, d.G_off, d.G_tet, ng, P, reinterpret_cast<const uint32_t*>(c->blk.p),
+                           static_cast<uint32_t*>(c->G_end.p));
+        HIPCHK(c, hipGetLastError());
+        d.G_end = static_cast<const uint32_t*>(c->G_end.p);
+    } else {
+        release(c->G_end);
+    }
+    HIPCHK(c, hipEventRecord(c->load_ev[1], s));
 
     // work-list sizes (exact: one record per F entry of a row genome)
     c->row_fprefix.assign(c->n_rows + 1, 0);
@@ -1085,7 +1107,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw, &c->srec_a, &c->srec_b, &c->shist,
                       &c->sgsum, &c->sbase})

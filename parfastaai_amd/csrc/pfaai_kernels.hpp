@@ -61,6 +61,7 @@ struct Dev {
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
     const uint32_t* G_pos;      // [|G|] F index of each G entry (all-vs-all; nullptr if not built)
+    const uint32_t* G_end;      // [|G|] end of the F run of each G entry (built with G_pos)
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
     const uint16_t* Fp16;       // [|F|] protein of each F entry, u16 (k_blk)
     const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)(d.n_f + 16) * 4u);
     const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
     // the run table: 16-B entries (k_blk), or u32 run ends under WK 3 (k_blk_end)
-    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * (WK == 3 ? 4u : 16u));  // < 4 GiB: P <= 1600 (host-checked)
+    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked); unused by WK 3
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);
     const rsrc_t r_t = mk_rsrc(d.T, (uint64_t)P * d.t_cols * 4u);
     // S1 / S2 return the raw loads: nothing may touch a prefetched value
@@ -297,11 +297,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // unconditional form for A/B)
     constexpr bool kSkip = (VAR & 64) == 0;
     const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
-    // WK 3: S1 also loads each entry's G_pos, S2 carries it on (gq -> gq2)
-    // and loads only the run's end (from k_blk_end's u32 table); S3 cuts [G_pos + 1, end) into 16-member
-    // tasks from an 8-aligned start (pl_issue_m2<A8>)
+    // WK 3: S1 loads each entry's G_pos and G_end (the end of its F run,
+    // built at load) -- two coalesced loads, no tetramer id and no run-table
+    // lookup; S2 only carries them on (gq -> gq2, gt -> r4.y); S3 cuts
+    // [G_pos + 1, G_end) into 16-member tasks from an 8-aligned start
+    // (pl_issue_m2<A8>)
     constexpr bool GP = WK == 3;
     const rsrc_t r_gp = mk_rsrc(GP ? d.G_pos + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
+    const rsrc_t r_ge = mk_rsrc(GP ? d.G_end + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
     auto s1 = [&](int p, int32_t (&gt)[EPT], uint32_t (&gq)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
         const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
         if constexpr (kSkip) {
@@ -310,8 +313,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
-            gt[j] = (int32_t)bld_u32(r_g, e < n ? e * 4u : kOOB, o * 4u);
-            if constexpr (GP) gq[j] = bld_u32(r_gp, e < n ? e * 4u : kOOB, o * 4u);
+            if constexpr (GP) {
+                gq[j] = bld_u32(r_gp, e < n ? e * 4u : kOOB, o * 4u);
+                gt[j] = (int32_t)bld_u32(r_ge, e < n ? e * 4u : kOOB, o * 4u);  // run end (0 past the list)
+            } else {
+                gt[j] = (int32_t)bld_u32(r_g, e < n ? e * 4u : kOOB, o * 4u);
+            }
         }
     };
     auto s2 = [&](int p, const int32_t (&gt)[EPT], uint4 (&r4)[EPT], const uint32_t (&gq)[EPT], uint32_t (&gq2)[EPT]) {
@@ -324,9 +331,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
             if constexpr (GP) {
+                (void)e;
                 gq2[j] = gq[j];
-                r4[j].y = bld_u32(r_blk, e < n ? (uint32_t)gt[j] * 4u : kOOB,
-                                  (uint32_t)min(p, P - 1) * (kNTetramers * 4u));
+                r4[j].y = (uint32_t)gt[j];  // G_end (S1)
             } else {
                 r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB,
                                  (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
