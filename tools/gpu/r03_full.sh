@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp PFAAI_PROGRESS=gpurun_out/progress.log
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -rf --timeout 600 --timeout-method thread \
+timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -rf --timeout 600 --timeout-method thread \
     > gpurun_out/pytest_full.log 2>&1 || { tail -40 gpurun_out/pytest_full.log; exit 1; }
 tail -3 gpurun_out/pytest_full.log
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --cpu-baseline none > gpurun_out/bench_full.json 2> gpurun_out/bench_full.log || { tail -5 gpurun_out/bench_full.log; exit 1; }
