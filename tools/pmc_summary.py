@@ -58,6 +58,12 @@ def derive(c):
         out["wave_frac_waiting"] = c.get("SQ_WAIT_ANY", 0) / w
         out["wave_frac_issue_stall"] = c.get("SQ_WAIT_INST_ANY", 0) / w
         out["wave_frac_active"] = c.get("SQ_ACTIVE_INST_ANY", 0) / w
+    if c.get("SQ_ACTIVE_INST_VALU", 0) > 0 and c.get("GRBM_GUI_ACTIVE", 0) > 0:
+        # SQ_ACTIVE_INST_* count quad-cycles summed over waves; GRBM_GUI_ACTIVE is
+        # the kernel's cycles summed over the 8 XCDs (MI355X_MICROARCH.md): the
+        # fraction of every SIMD's cycles issuing VALU (1024 SIMDs)
+        out["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (c["GRBM_GUI_ACTIVE"] / 8)
+        out["kernel_cycles"] = c["GRBM_GUI_ACTIVE"] / 8
     if c.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
         out["lds_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
     return out
@@ -82,6 +88,10 @@ def main():
         with open(os.path.join(prof, "pmc_k_rows.json"), "w") as f:
             json.dump({"kernel": k, "hbm_bytes_per_launch": dv.get("hbm_bytes"),
                        "hbm_read_bytes_x2_bound": dv.get("hbm_read_bytes_x2_bound"),
+                       "valu_busy": dv.get("valu_busy"), "wave_frac_waiting": dv.get("wave_frac_waiting"),
+                       "lds_conflict_frac": dv.get("lds_conflict_frac"),
+                       "valu_insts": res[k]["counters"].get("SQ_INSTS_VALU"),
+                       "salu_insts": res[k]["counters"].get("SQ_INSTS_SALU"),
                        "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, one launch covers all 10k rows",
                        "tag": tag}, f, indent=1)
     for k, v in res.items():
