@@ -175,7 +175,7 @@ inline int write_csv(const std::string& path, const std::vector<std::string>& ro
 template <typename JAC>
 inline int write_bin(const std::string& prefix, const std::vector<JAC>& jac, const std::vector<double>& aji,
                      const std::vector<double>& M, int64_t rows, int64_t cols) {
-    auto put = [](FILE* f, const void* p, std::size_t n) { return std::fwrite(p, 1, n, f) == n; };
+    auto put = [](FILE* f, const void* p, std::size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; };  // (empty vectors: data() may be null)
     bool ok = true;
     if (FILE* f = std::fopen((prefix + "_jac.bin").c_str(), "wb")) {
         uint64_t n = jac.size();

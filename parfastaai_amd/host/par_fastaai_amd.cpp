@@ -235,7 +235,7 @@ double ms_since(std::chrono::steady_clock::time_point t) {
 // --dump-arrays: the loader's arrays in the reference's fixture format
 // (vector<int> Lc, vector<DPair<int,int>> F, DMatrix<int> T), no GPU.
 int dump_arrays(const std::string& prefix, const LoadedArrays& arr) {
-    auto put = [](FILE* f, const void* p, std::size_t n) { return std::fwrite(p, 1, n, f) == n; };
+    auto put = [](FILE* f, const void* p, std::size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; };  // (empty vectors: data() may be null)
     bool ok = true;
     if (FILE* f = std::fopen((prefix + "_lc_array.bin").c_str(), "wb")) {
         uint64_t n = arr.Lc.size();
@@ -258,7 +258,7 @@ int dump_arrays(const std::string& prefix, const LoadedArrays& arr) {
 // --dump-genomes: the G-path arrays (cereal vector<int64> G_off, vector<int>
 // G_tet, DMatrix<int> T), no GPU.
 int dump_genomes(const std::string& prefix, const LoadedArrays& arr) {
-    auto put = [](FILE* f, const void* p, std::size_t n) { return std::fwrite(p, 1, n, f) == n; };
+    auto put = [](FILE* f, const void* p, std::size_t n) { return n == 0 || std::fwrite(p, 1, n, f) == n; };  // (empty vectors: data() may be null)
     bool ok = true;
     if (FILE* f = std::fopen((prefix + "_g_off.bin").c_str(), "wb")) {
         uint64_t n = arr.G_off.size();
