@@ -89,7 +89,8 @@ __global__ void k_rowptr(const uint32_t* __restrict__ keys, int64_t n, int64_t K
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const int64_t k = keys[j];
-    const int64_t kp = j > 0 ? (int64_t)keys[j - 1] : -1;
+    const int64_t kq = keys[j > 0 ? j - 1 : 0];  // (unconditional: no wait at a branch)
+    const int64_t kp = j > 0 ? kq : -1;
     for (int64_t x = kp + 1; x <= k; ++x) rowptr[x] = (unsigned long long)j;
     if (j == n - 1)
         for (int64_t x = k + 1; x <= K; ++x) rowptr[x] = (unsigned long long)n;

@@ -154,8 +154,23 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
     for (int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < n_lists; q += waves) {
         const int64_t p = q / n_ids, L = (q - p * n_ids) * P + p;
         const int64_t row = p * kNTetramers;
-        const int64_t e = G_off[L + 1];
-        for (int64_t k = G_off[L] + lane; k < e; k += 64) G_end[k] = ends[row + G_tet[k]];
+        const int64_t b = G_off[L], e = G_off[L + 1];
+        // four 64-entry chunks per round: every G_tet load, then every table
+        // lookup, then the stores (a list is ~290 entries at 10k: two rounds
+        // of two dependent loads instead of five)
+        // (indices clamped into the list rather than loads under a branch,
+        // which the compiler waits for at the branch)
+        for (int64_t k0 = b + lane; k0 < e; k0 += 4 * 64) {
+            int32_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = G_tet[min(k0 + u * 64, e - 1)];
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = ends[row + t[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u * 64 < e) G_end[k0 + u * 64] = v[u];
+        }
     }
 }
 

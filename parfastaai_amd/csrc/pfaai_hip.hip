@@ -178,7 +178,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
     if (ends) {  // k_rows_pl WK 3 reads run ends only (pl_uses_ends)
         const char* et = DIAG_ENV("PFAAI_BLK_END_TILE");  // tetramers per workgroup (A/B)
         const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(et ? std::min(atoi(et), kBlkEndTileMax) : kBlkEndTileMax,
-                                                                     kBlkLdsBytes / (4 * c->prob.n_prot)));
+                                                                     kBlkEndDynLds / (4 * c->prob.n_prot)));
         const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint32_t);
         const char* eu = DIAG_ENV("PFAAI_BLK_END_U");  // loads in flight per lane (A/B)
         const int u = eu ? atoi(eu) : 1;
@@ -195,7 +195,7 @@ int build_runs_g(pfaai_ctx* c, hipStream_t s, bool first_event, bool ends) {
         HIPCHK(c, hipGetLastError());
         return PFAAI_RC_OK;
     }
-    const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * c->prob.n_prot)));
+    const int tile = (int)std::max<int64_t>(1, std::min<int64_t>(kBlkTileMax, kBlkDynLds / (16 * c->prob.n_prot)));
     const int dbg = DIAG_ENV("PFAAI_BLK_ABLATE") ? atoi(DIAG_ENV("PFAAI_BLK_ABLATE")) : 0;
     const size_t lds = (size_t)c->prob.n_prot * tile * sizeof(uint4);
     // 1024 threads (0.649 vs 0.666 ms at 10k; the window form gains 2x, see
@@ -275,9 +275,9 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
         c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
                      !(wv && wv[0] == '0') &&
                      (int64_t)c->cols_run + 1 > wcols;
-        if (c->windows) {  // all windows' tables staged in one k_blk workgroup's 80 KB of LDS (nwin * P <= 5120)
+        if (c->windows) {  // all windows' tables staged in one k_blk workgroup's LDS (nwin * P <= 5104)
             nwin = (int)ceil_div(MODE == 2 ? c->prob.n_tgt : c->prob.n_ids, wcols);
-            win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkLdsBytes / (16 * (int64_t)c->prob.n_prot * nwin));
+            win_tile = (int)std::min<int64_t>(kBlkTileMax, kBlkDynLds / (16 * (int64_t)c->prob.n_prot * nwin));
             c->windows = win_tile >= 1 &&
                          ensure(c, c->blkw, (size_t)nwin * c->prob.n_prot * kNTetramers * sizeof(uint4)) == PFAAI_RC_OK;
         }
@@ -466,7 +466,7 @@ int ensure_tsort(pfaai_ctx* c, int64_t n, int kb, bool keygen) {
     int passes;
     const int db = tsort_db(kb, &passes);
     const int64_t nn = std::max<int64_t>(n, 1);
-    const int64_t ntiles = ceil_div(nn, kSortTile), ngroups = ceil_div(ntiles, kSortGroup);
+    const int64_t ntiles = ceil_div(nn, kSortTileMin), ngroups = ceil_div(ntiles, kSortGroup);
     int rc;
     if ((rc = ensure(c, c->srec_a, nn * 8)) || ((keygen || passes > 2) && (rc = ensure(c, c->srec_b, nn * 8))) ||
         (rc = ensure(c, c->shist, (size_t)ntiles * (4u << db))) ||
@@ -480,20 +480,20 @@ int ensure_scan(pfaai_ctx* c, int64_t n) {
     return ensure(c, c->sums, std::max<int64_t>(1, ceil_div(std::max<int64_t>(n, PFAAI_NTETRAMERS), kScanTile)) * 8);
 }
 
-template <int DB, class S0, class DN>
+template <int DB, int NT, bool PF, class S0, class DN, int VAR = 0>
 void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, int passes, hipStream_t s) {
-    const int64_t ntiles = ceil_div(n, kSortTile), ngroups = ceil_div(ntiles, kSortGroup);
+    const int64_t ntiles = ceil_div(n, sort_tile<NT>()), ngroups = ceil_div(ntiles, kSortGroup);
     auto* hist = static_cast<uint32_t*>(c->shist.p);
     auto* gsum = static_cast<uint32_t*>(c->sgsum.p);
     auto* base = static_cast<uint32_t*>(c->sbase.p);
     uint64_t* buf[2] = {static_cast<uint64_t*>(c->srec_a.p), static_cast<uint64_t*>(c->srec_b.p)};
-    const size_t lds = sort_scatter_lds<DB>();
-    // persistent scatter: one 1024-thread workgroup per CU (its LDS tile and
-    // counters take ~104 KB of the 160), each walking ntiles / grid tiles
+    const size_t lds = sort_scatter_lds<DB, NT>();
+    // persistent scatter: as many workgroups as fit the CUs (two 512-thread
+    // ones per CU at DB <= 10), each walking ntiles / grid tiles
     int cus = 256, per_cu = 1;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_sort_scatter<DB, SrcRecs, DstRecs>),
-                                                       kSortThreads, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&k_sort_scatter<DB, NT, PF, SrcRecs, DstRecs>), NT, lds);
     const int grid = (int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per_cu));
     for (int pass = 0; pass < passes; ++pass) {
         const int shift = pass * DB;
@@ -503,16 +503,15 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
         const SrcRecs prev{buf[(pass + 1) & 1]};  // pass p reads what pass p - 1 wrote
         const DstRecs next{buf[pass & 1]};
         if (pass == 0)
-            hipLaunchKernelGGL((k_sort_hist<DB, S0>), dim3(ntiles), dim3(kSortThreads), 0, s, src0, n, shift, mask,
-                               hist);
+            hipLaunchKernelGGL((k_sort_hist<DB, NT, S0>), dim3(ntiles), dim3(NT), 0, s, src0, n, shift, mask, hist);
         else
-            hipLaunchKernelGGL((k_sort_hist<DB, SrcRecs>), dim3(ntiles), dim3(kSortThreads), 0, s, prev, n, shift,
-                               mask, hist);
+            hipLaunchKernelGGL((k_sort_hist<DB, NT, SrcRecs>), dim3(ntiles), dim3(NT), 0, s, prev, n, shift, mask,
+                               hist);
         hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
         hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base);
 #define SC(SRC_T, SRC, DST_T, DST)                                                                        \
-    hipLaunchKernelGGL((k_sort_scatter<DB, SRC_T, DST_T>), dim3(grid), dim3(kSortThreads), lds, s, SRC, DST, n, \
-                       ntiles, shift, mask, hist, gsum, base)
+    hipLaunchKernelGGL((k_sort_scatter<DB, NT, PF, SRC_T, DST_T, VAR>), dim3(grid), dim3(NT), lds, s, SRC, DST, n, ntiles, \
+                       shift, mask, hist, gsum, base)
         if (pass == 0 && last) SC(S0, src0, DN, dstN);
         else if (pass == 0) SC(S0, src0, DstRecs, next);
         else if (last) SC(SrcRecs, prev, DN, dstN);
@@ -531,14 +530,43 @@ int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipSt
     // the ping-pong buffers this pass count writes (ensure_tsort sized them
     // from the same tsort_db): pass p writes srec[p & 1] except the last
     const size_t need = (size_t)n * 8;
-    if (c->srec_a.bytes < need || c->shist.bytes < (size_t)ceil_div(n, kSortTile) * (4u << db) ||
+    if (c->srec_a.bytes < need || c->shist.bytes < (size_t)ceil_div(n, kSortTileMin) * (4u << db) ||
         (passes > 2 && c->srec_b.bytes < need))
         return fail(c, PFAAI_RC_INVALID, "internal: transposition sort buffers not sized for this pass count");
+#ifdef PFAAI_DIAGNOSTICS
+    // diagnostics (A/B): PFAAI_TSORT_NT=1024 the one-per-CU form (with the
+    // next-tile prefetch), PFAAI_TSORT_PF=0|1 the prefetch of the 512 form
+    const char* nt = DIAG_ENV("PFAAI_TSORT_NT");
+    const char* pf = DIAG_ENV("PFAAI_TSORT_PF");
+    if (const char* vr = DIAG_ENV("PFAAI_TSORT_VAR"); vr && db == 10) {  // scatter variants / ablations (A/B)
+        switch (atoi(vr)) {
+            case 1: tsort_launch<10, kSortNT, kSortPF, S0, DN, 1>(c, src0, dstN, n, kb, passes, s); break;
+            case 3: tsort_launch<10, kSortNT, kSortPF, S0, DN, 3>(c, src0, dstN, n, kb, passes, s); break;
+            case 5: tsort_launch<10, kSortNT, kSortPF, S0, DN, 5>(c, src0, dstN, n, kb, passes, s); break;
+            case 9: tsort_launch<10, kSortNT, kSortPF, S0, DN, 9>(c, src0, dstN, n, kb, passes, s); break;
+            case 13: tsort_launch<10, kSortNT, kSortPF, S0, DN, 13>(c, src0, dstN, n, kb, passes, s); break;
+            default: tsort_launch<10, kSortNT, kSortPF, S0, DN, 0>(c, src0, dstN, n, kb, passes, s); break;
+        }
+        HIPCHK(c, hipGetLastError());
+        return PFAAI_RC_OK;
+    }
+    if ((nt && atoi(nt) == 1024) || (pf && (atoi(pf) != 0) != kSortPF)) {
+        const bool big = nt && atoi(nt) == 1024;
+        switch (db) {
+            case 8: big ? tsort_launch<8, 1024, true>(c, src0, dstN, n, kb, passes, s) : tsort_launch<8, kSortNT, !kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+            case 9: big ? tsort_launch<9, 1024, true>(c, src0, dstN, n, kb, passes, s) : tsort_launch<9, kSortNT, !kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+            case 10: big ? tsort_launch<10, 1024, true>(c, src0, dstN, n, kb, passes, s) : tsort_launch<10, kSortNT, !kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+            default: big ? tsort_launch<11, 1024, true>(c, src0, dstN, n, kb, passes, s) : tsort_launch<11, kSortNT, !kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+        }
+        HIPCHK(c, hipGetLastError());
+        return PFAAI_RC_OK;
+    }
+#endif
     switch (db) {
-        case 8: tsort_launch<8>(c, src0, dstN, n, kb, passes, s); break;
-        case 9: tsort_launch<9>(c, src0, dstN, n, kb, passes, s); break;
-        case 10: tsort_launch<10>(c, src0, dstN, n, kb, passes, s); break;
-        default: tsort_launch<11>(c, src0, dstN, n, kb, passes, s); break;
+        case 8: tsort_launch<8, kSortNT, kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+        case 9: tsort_launch<9, kSortNT, kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+        case 10: tsort_launch<10, kSortNT, kSortPF>(c, src0, dstN, n, kb, passes, s); break;
+        default: tsort_launch<11, kSortNT, kSortPF>(c, src0, dstN, n, kb, passes, s); break;
     }
     HIPCHK(c, hipGetLastError());
     return PFAAI_RC_OK;

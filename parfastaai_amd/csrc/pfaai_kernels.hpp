@@ -286,7 +286,10 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
 //             holding A, i.e. its E triples (ds_helper.hpp:270-357).
 // ---------------------------------------------------------------------------
 constexpr int kBlkTileMax = 16;        // tetramers per k_blk workgroup (fewer for many proteins)
-constexpr int kBlkLdsBytes = 80 << 10;  // its LDS staging: n_prot x tile x 16 B (two workgroups share a CU's 160 KB)
+constexpr int kBlkLdsBytes = 80 << 10;  // LDS per workgroup (two workgroups share a CU's 160 KB)
+// k_blk's dynamic staging (n_prot x tile x 16 B) gets what its static LDS
+// (lp[]) leaves of kBlkLdsBytes, so two workgroups still fit a CU at any P
+constexpr int kBlkDynLds = kBlkLdsBytes - 256;
 
 // dbg: bit 0 skips (1), bit 1 (2), bit 2 (3) -- PFAAI_BLK_ABLATE (diagnostics) and, for
 // query-vs-target window tables, bit 1 (no splitters: nothing there prunes by them).
@@ -431,6 +434,11 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
 // writes 4 B per (protein, tetramer) slot -- a quarter of k_blk's table, and
 // no pass over Fg.
 constexpr int kBlkEndTileMax = 64;
+constexpr int kBlkEndGranMax = 8192;  // granule table entries (u8)
+// the dynamic staging's share of kBlkLdsBytes: k_blk_end's static LDS (the
+// granule table and lp[]) comes first -- at n_prot >= 320 a full 80 KB of
+// staging on top of it left room for one workgroup per CU
+constexpr int kBlkEndDynLds = kBlkLdsBytes - kBlkEndGranMax - (kBlkEndTileMax + 1) * 8 - 64;
 
 template <int NTH, int U = 1>
 __global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
@@ -441,7 +449,7 @@ __global__ __launch_bounds__(NTH, 2048 / 256) void k_blk_end(Dev d, int tile) {
     // LDS read per 8-entry chunk instead of a 6-step binary search (a chain
     // of dependent LDS reads) -- tiles with more granules (a tetramer held by
     // most genomes) keep the search
-    constexpr int kGran = 6, kGranMax = 8192;
+    constexpr int kGran = 6, kGranMax = kBlkEndGranMax;
     __shared__ uint8_t gtl[kGranMax];
     const int tid = threadIdx.x, lane = tid & 63, P = d.n_prot;
     const int t0 = blockIdx.x * tile;

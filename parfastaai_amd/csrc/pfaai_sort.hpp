@@ -10,7 +10,8 @@
 //   F from G   the G entries enumerated protein-major, key t (18 bits): a
 //              stable sort by tetramer leaves each (t, p) run in genome order
 //
-// Per pass (digit of DB bits, BINS = 2^DB; tiles of kSortTile = 8192 records):
+// Per pass (digit of DB bits, BINS = 2^DB; tiles of NT * kSortItems records,
+// NT = kSortNT threads: 4096 records at the default 512):
 //   k_sort_hist    per-tile digit counts -> hist[tile][bin] (tile-major, one
 //                  coalesced 4-KB row per tile at DB = 10)
 //   k_sort_grp     per group of kSortGroup tiles: hist rows -> exclusive prefix
@@ -33,11 +34,20 @@
 
 namespace pfaai {
 
-constexpr int kSortThreads = 1024;
+constexpr int kSortThreads = 1024;                      // k_sort_grp / k_sort_top
 constexpr int kSortItems = 8;                           // records per thread and tile
-constexpr int kSortTile = kSortThreads * kSortItems;    // 8192
+// threads of the hist / scatter workgroups: 512 (tiles of 4096 records; the
+// scatter's LDS, 56 KB at 10-bit digits, lets two workgroups share a CU, so
+// one's barriers and write-phase loads overlap the other's ranking) -- one
+// 1024-thread workgroup per CU (8192-record tiles, ~104 KB of LDS) left the
+// CU idle at every barrier: 2.9-3.3 ms per pass at 10k, ~1.5 TB/s
+constexpr int kSortNT = 512;
+constexpr bool kSortPF = false;                          // next-tile prefetch (k_sort_scatter PF)
+constexpr int kSortTileMin = 512 * kSortItems;          // the smallest tile (sizes the hist buffer)
 constexpr int kSortGroup = 128;                         // tiles per group of the hist scan
 constexpr int kSortMaxDB = 11;
+template <int NT>
+constexpr int sort_tile() { return NT * kSortItems; }
 
 __device__ __forceinline__ uint32_t sort_digit(uint64_t r, int shift, uint32_t mask) {
     return (uint32_t)(r >> shift) & mask;
@@ -52,9 +62,9 @@ struct SrcFKeys {
     const int32_t* Fg;
     uint32_t P;
     uint16_t* fp16;  // nullable
-    __device__ __forceinline__ uint64_t hist_rec(int64_t i) const {
+    __device__ __forceinline__ uint64_t hist_rec(int64_t i, bool valid) const {
         const int32_t p = Fp[i], g = Fg[i];
-        if (fp16) fp16[i] = (uint16_t)p;
+        if (fp16 && valid) fp16[i] = (uint16_t)p;
         return (uint64_t)((uint32_t)g * P + (uint32_t)p);
     }
     __device__ __forceinline__ uint64_t load(int64_t i) const {
@@ -65,7 +75,7 @@ struct SrcFKeys {
 // materialised records (later passes; first passes of the keygen paths)
 struct SrcRecs {
     const uint64_t* r;
-    __device__ __forceinline__ uint64_t hist_rec(int64_t i) const { return r[i]; }
+    __device__ __forceinline__ uint64_t hist_rec(int64_t i, bool) const { return r[i]; }
     __device__ __forceinline__ uint64_t load(int64_t i) const { return r[i]; }
 };
 
@@ -76,6 +86,7 @@ struct SrcRecs {
 
 struct DstRecs {
     uint64_t* r;
+    static constexpr int kWH = kSortItems;
     static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
@@ -116,6 +127,7 @@ struct DstGposHash {
     uint64_t seed;
     int* err;
     unsigned long long* sum;
+    static constexpr int kWH = kSortItems;
     static constexpr bool kSum = true;
     struct Aux {
         uint32_t lo, hi;  // list bounds (< 2^32: |G| = |F| <= 2^32 - 64)
@@ -159,6 +171,7 @@ struct DstGFromRecs {
     const int64_t* Lp;
     int kb;
     int* err;
+    static constexpr int kWH = kSortItems / 2;  // (three-field Aux: eight in flight spill)
     static constexpr bool kSum = false;
     struct Aux {
         uint32_t lo, hi, lp;  // (all < 2^32: |F| <= 2^32 - 64)
@@ -189,6 +202,7 @@ struct DstFFromG {
     int32_t* Fg;
     uint16_t* fp16;
     uint32_t* Ft;
+    static constexpr int kWH = kSortItems;
     static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
@@ -204,25 +218,30 @@ struct DstFFromG {
 
 // ---- the pass kernels -------------------------------------------------------
 
-template <int DB, class Src>
-__global__ __launch_bounds__(kSortThreads) void k_sort_hist(Src src, int64_t n, int shift, uint32_t mask,
-                                                            uint32_t* __restrict__ hist) {
+template <int DB, int NT, class Src>
+__global__ __launch_bounds__(NT) void k_sort_hist(Src src, int64_t n, int shift, uint32_t mask,
+                                                  uint32_t* __restrict__ hist) {
     constexpr int BINS = 1 << DB;
     __shared__ uint32_t h[BINS];
-    for (int b = threadIdx.x; b < BINS; b += kSortThreads) h[b] = 0u;
+    for (int b = threadIdx.x; b < BINS; b += NT) h[b] = 0u;
     __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * kSortTile;
+    const int64_t t0 = (int64_t)blockIdx.x * sort_tile<NT>();
     uint32_t d[kSortItems];
+    // every load issued before the first LDS atomic, none under a branch: a
+    // load in a branch is waited for before the branch joins (vmcnt(0)), so
+    // a conditional load per item serialised eight HBM round trips
 #pragma unroll
-    for (int k = 0; k < kSortItems; ++k) {  // every load issued before the first LDS atomic
-        const int64_t i = t0 + k * kSortThreads + threadIdx.x;
-        d[k] = i < n ? sort_digit(src.hist_rec(i), shift, mask) : 0xFFFFFFFFu;
+    for (int k = 0; k < kSortItems; ++k) {
+        const int64_t i = t0 + k * NT + threadIdx.x;
+        const bool valid = i < n;
+        d[k] = sort_digit(src.hist_rec(valid ? i : n - 1, valid), shift, mask);
+        if (!valid) d[k] = 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; ++k)
         if (d[k] != 0xFFFFFFFFu) atomicAdd(&h[d[k]], 1u);
     __syncthreads();
-    for (int b = threadIdx.x; b < BINS; b += kSortThreads) hist[(int64_t)blockIdx.x * BINS + b] = h[b];
+    for (int b = threadIdx.x; b < BINS; b += NT) hist[(int64_t)blockIdx.x * BINS + b] = h[b];
 }
 
 // hist rows of one group of tiles -> exclusive prefix within the group (in
@@ -310,26 +329,40 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_top(uint32_t* __restrict_
     }
 }
 
-// dynamic LDS of k_sort_scatter<DB>
-template <int DB>
+// dynamic LDS of k_sort_scatter<DB, NT>
+template <int DB, int NT>
 constexpr size_t sort_scatter_lds() {
-    return (size_t)(kSortThreads / 64) * (1 << DB) * 2   // per-wave u16 digit counters
-           + 2 * (size_t)(1 << DB) * 4                    // lstart, gbase
-           + (size_t)kSortTile * 8;                       // the reordered tile
+    return (size_t)(NT / 64) * (1 << DB) * 2   // per-wave u16 digit counters
+           + 2 * (size_t)(1 << DB) * 4          // lstart, gbase
+           + (size_t)sort_tile<NT>() * 8;       // the reordered tile
 }
 
-template <int DB, class Src, class Dst>
-__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst, int64_t n, int64_t ntiles, int shift,
-                                                               uint32_t mask, const uint32_t* __restrict__ hist,
-                                                               const uint32_t* __restrict__ gsum,
-                                                               const uint32_t* __restrict__ binbase) {
-    constexpr int BINS = 1 << DB, W = kSortThreads / 64;
-    constexpr int BPT = BINS > kSortThreads ? BINS / kSortThreads : 1;  // digits per thread (scans)
+// waves per SIMD the scatter is compiled for: two 512-thread workgroups per
+// CU (<= 128 VGPRs)
+template <int NT>
+constexpr int sort_scatter_wpe() { return NT == 512 ? 4 : 1; }
+
+// PF: the next tile's records and digit bases are loaded while this tile is
+// ranked and written (16 + BPT VGPRs live across the tile)
+// VAR (diagnostics A/B, 0 in the product): bit 0 round-robin tile order,
+// bit 1 the ranking ballots done twice (their cost), bit 2 records stored straight
+// from registers at their ranked positions (no LDS reorder), bit 3 no global
+// stores (ablation)
+template <int DB, int NT, bool PF, class Src, class Dst, int VAR = 0>
+__global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
+    Src src, Dst dst, int64_t n, int64_t ntiles, int shift, uint32_t mask, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ gsum, const uint32_t* __restrict__ binbase) {
+    constexpr int BINS = 1 << DB, W = NT / 64, kTile = sort_tile<NT>();
+    constexpr int BPT = BINS > NT ? BINS / NT : 1;  // digits per thread (scans)
+    // write phase: Dst::kWH records' destination loads issued before the
+    // first store -- all eight where the registers allow (gfx9 counts stores
+    // in vmcnt: a second batch's loads wait for the first batch's stores)
+    constexpr int kWH = Dst::kWH;
     extern __shared__ __align__(16) unsigned char sort_lds[];
-    uint64_t* srt = reinterpret_cast<uint64_t*>(sort_lds);                              // [kSortTile]
-    uint32_t* lstart = reinterpret_cast<uint32_t*>(sort_lds + (size_t)kSortTile * 8);  // [BINS]
-    uint32_t* gbase = lstart + BINS;                                                    // [BINS]
-    uint16_t* cnt = reinterpret_cast<uint16_t*>(gbase + BINS);                          // [W][BINS]
+    uint64_t* srt = reinterpret_cast<uint64_t*>(sort_lds);                          // [kTile]
+    uint32_t* lstart = reinterpret_cast<uint32_t*>(sort_lds + (size_t)kTile * 8);  // [BINS]
+    uint32_t* gbase = lstart + BINS;                                                // [BINS]
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(gbase + BINS);                      // [W][BINS], 16-B aligned
     __shared__ uint32_t wsum[W];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -341,36 +374,56 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
     // ranks and writes tile j.
     uint64_t rec[kSortItems];
     uint32_t gb[BPT];
+    // the tile's loads are unconditional (indices clamped into range: a load
+    // under a branch is waited for at the branch, which serialised the eight
+    // record loads of a tile -- ~2.8 ms per pass at 10k); records past n are
+    // never used (every use below checks the position)
     auto fetch_tile = [&](int64_t tile, uint64_t (&r)[kSortItems], uint32_t (&g)[BPT]) {
-        const int64_t t0 = tile * kSortTile;
+        const int64_t tc = tile < ntiles ? tile : ntiles - 1;
+        const int64_t t0 = tc * kTile;
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
             const int64_t i = t0 + (wid * kSortItems + k) * 64 + lane;
-            r[k] = (tile < ntiles && i < n) ? src.load(i) : 0ull;
+            r[k] = src.load(i < n ? i : n - 1);
         }
-        const int64_t grp = tile / kSortGroup;
+        const int64_t grp = tc / kSortGroup;
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
-            const int b = tid + q * kSortThreads;
-            g[q] = (tile < ntiles && b < BINS) ? binbase[b] + gsum[grp * BINS + b] + hist[tile * BINS + b] : 0u;
+            const int b = min(tid + q * NT, BINS - 1);
+            g[q] = binbase[b] + gsum[grp * BINS + b] + hist[tc * BINS + b];
         }
     };
     uint64_t hsum = 0;  // Dst::kSum: the destination's per-record sum (DstGposHash)
-    fetch_tile(blockIdx.x, rec, gb);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kSortTile;
+    // tile order: tile0 + j * tstep.  The workgroups of one XCD (blockIdx %
+    // 8: dispatch is round-robin over the 8 XCDs) walk one contiguous eighth
+    // of the tiles, so the tiles in flight on an XCD write adjacent pieces of
+    // every digit's output run, and whole lines leave its L2 (round-robin
+    // tiles: 2.72 -> 2.32 ms for the 10k F -> G first pass); VAR bit 0 keeps
+    // the round-robin order (A/B)
+    int64_t tile0 = blockIdx.x, tstep = gridDim.x, tend = ntiles;
+    if constexpr ((VAR & 1) == 0) {
+        const int64_t nx = gridDim.x / 8, x = blockIdx.x % 8;
+        if (nx >= 1 && (int64_t)gridDim.x % 8 == 0) {
+            const int64_t per = (ntiles + 7) / 8;
+            tile0 = x * per + blockIdx.x / 8;
+            tstep = nx;
+            tend = min(ntiles, (x + 1) * per);
+        }
+    }
+    fetch_tile(tile0 < tend ? tile0 : ntiles, rec, gb);
+    for (int64_t tile = tile0; tile < tend; tile += tstep) {
+        const int64_t t0 = tile * kTile;
+        const int64_t tnext = tile + tstep < tend ? tile + tstep : ntiles;
         uint64_t nrec[kSortItems];
         uint32_t ngb[BPT];
-        fetch_tile(tile + gridDim.x, nrec, ngb);  // in flight during this tile
+        if constexpr (PF) fetch_tile(tnext, nrec, ngb);  // in flight during this tile
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
-            const int b = tid + q * kSortThreads;
-            if (b < BINS) {
-                gbase[b] = gb[q];
-#pragma unroll
-                for (int w = 0; w < W; ++w) cnt[w * BINS + b] = 0;
-            }
+            const int b = tid + q * NT;
+            if (b < BINS) gbase[b] = gb[q];
         }
+        // the per-wave counters cleared by 16-B stores (W * BINS / 8 of them)
+        for (int x = tid; x < W * BINS / 8; x += NT) reinterpret_cast<uint4*>(cnt)[x] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         uint16_t lr[kSortItems];
 #pragma unroll
@@ -383,6 +436,18 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
                 const bool on = (d >> bit) & 1u;
                 const uint64_t m = __ballot(on);
                 peers &= on ? m : ~m;
+            }
+            if constexpr ((VAR & 2) != 0) {  // the ballots a second time (their cost, by difference)
+                uint64_t p2 = __ballot(valid);
+                uint32_t d2 = d;
+                asm volatile("" : "+v"(d2));  // opaque: the ballots are not folded into the first set
+#pragma unroll
+                for (int bit = 0; bit < DB; ++bit) {
+                    const bool on = (d2 >> bit) & 1u;
+                    const uint64_t m = __ballot(on);
+                    p2 &= on ? m : ~m;
+                }
+                peers = p2;
             }
             const uint32_t r = (uint32_t)__popcll(peers & lt), c = (uint32_t)__popcll(peers);
             const uint32_t base = valid ? wc[d] : 0u;
@@ -425,42 +490,76 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(Src src, Dst dst,
             off += tot[q];
         }
         __syncthreads();
+        if constexpr ((VAR & 4) != 0) {  // straight from registers: position gbase + wave prefix + rank
 #pragma unroll
-        for (int k = 0; k < kSortItems; ++k) {
-            if (t0 + (wid * kSortItems + k) * 64 + lane < n) {
-                const uint32_t d = sort_digit(rec[k], shift, mask);
-                srt[lstart[d] + cnt[wid * BINS + d] + lr[k]] = rec[k];
+            for (int k = 0; k < kSortItems; ++k) {
+                if (t0 + (wid * kSortItems + k) * 64 + lane < n) {
+                    const uint32_t d = sort_digit(rec[k], shift, mask);
+                    const uint32_t pos = gbase[d] + cnt[wid * BINS + d] + lr[k];
+                    const auto ax = dst.fetch(pos, rec[k]);
+                    if constexpr ((VAR & 8) == 0) hsum += dst.store(pos, rec[k], ax);
+                }
             }
+            __syncthreads();
+            if constexpr (PF) {
+#pragma unroll
+                for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
+#pragma unroll
+                for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
+            } else {
+                fetch_tile(tnext, rec, gb);
+            }
+            continue;
+        }
+        {
+            uint32_t slot[kSortItems];  // every LDS read issued before the first write
+#pragma unroll
+            for (int k = 0; k < kSortItems; ++k) {
+                const uint32_t d = sort_digit(rec[k], shift, mask);
+                slot[k] = lstart[d] + cnt[wid * BINS + d] + lr[k];
+            }
+#pragma unroll
+            for (int k = 0; k < kSortItems; ++k)
+                if (t0 + (wid * kSortItems + k) * 64 + lane < n) srt[slot[k]] = rec[k];
         }
         __syncthreads();
         // write the tile in digit order: each digit's run is contiguous in the output
         // (positions are < 2^32: n <= 2^32 - 64; records re-read from LDS for the stores)
-        const int tn = (int)((n - t0) < kSortTile ? (n - t0) : kSortTile);
+        const int tn = (int)((n - t0) < kTile ? (n - t0) : kTile);
+        // (unconditional reads at positions clamped into the tile: no wait per item)
 #pragma unroll
-        for (int h = 0; h < kSortItems; h += kSortItems / 2) {  // two halves: fewer live registers
-            uint32_t pos[kSortItems / 2];
-            typename Dst::Aux aux[kSortItems / 2];
+        for (int h = 0; h < kSortItems; h += kWH) {  // kWH records per thread in flight
+            uint32_t pos[kWH];
+            uint64_t val[kWH];
+            typename Dst::Aux aux[kWH];
 #pragma unroll
-            for (int k = 0; k < kSortItems / 2; ++k) {
-                const int lp = tid + (h + k) * kSortThreads;
-                if (lp < tn) {
-                    const uint64_t v = srt[lp];
-                    const uint32_t d = sort_digit(v, shift, mask);
-                    pos[k] = gbase[d] + (uint32_t)(lp - (int)lstart[d]);
-                    aux[k] = dst.fetch(pos[k], v);
-                }
+            for (int k = 0; k < kWH; ++k) {
+                const int lp = min(tid + (h + k) * NT, tn - 1);
+                val[k] = srt[lp];
             }
 #pragma unroll
-            for (int k = 0; k < kSortItems / 2; ++k) {
-                const int lp = tid + (h + k) * kSortThreads;
-                if (lp < tn) hsum += dst.store(pos[k], srt[lp], aux[k]);
+            for (int k = 0; k < kWH; ++k) {
+                const int lp = min(tid + (h + k) * NT, tn - 1);
+                const uint32_t d = sort_digit(val[k], shift, mask);
+                pos[k] = gbase[d] + (uint32_t)(lp - (int)lstart[d]);
+            }
+#pragma unroll
+            for (int k = 0; k < kWH; ++k) aux[k] = dst.fetch(pos[k], val[k]);
+#pragma unroll
+            for (int k = 0; k < kWH; ++k) {
+                const int lp = tid + (h + k) * NT;
+                if ((VAR & 8) == 0 && lp < tn) hsum += dst.store(pos[k], val[k], aux[k]);
             }
         }
         __syncthreads();  // the LDS tile, counters and bases are rewritten by the next tile
+        if constexpr (PF) {
 #pragma unroll
-        for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
+            for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
 #pragma unroll
-        for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
+            for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
+        } else {
+            fetch_tile(tnext, rec, gb);
+        }
     }
     if constexpr (Dst::kSum) {
 #pragma unroll
@@ -480,11 +579,24 @@ __global__ __launch_bounds__(256) void k_fkeys_rec(const int64_t* __restrict__ L
                                                    uint64_t* __restrict__ rec, uint16_t* __restrict__ fp16) {
     for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
         const int64_t s = Lp[t], e = Lp[t + 1];
-        for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-            const int32_t p = Fp[i];
-            fp16[i] = (uint16_t)p;
-            rec[i] = (uint64_t)((uint32_t)Fg[i] * P + (uint32_t)p) | ((uint64_t)t << kb) |
-                     ((uint64_t)(i - s) << (kb + 18));
+        // four rounds of the workgroup per batch, loads first (clamped, not branched)
+        for (int64_t i0 = s + threadIdx.x; i0 < e; i0 += 4 * (int64_t)blockDim.x) {
+            int32_t p[4], g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = min(i0 + u * (int64_t)blockDim.x, e - 1);
+                p[u] = Fp[i];
+                g[u] = Fg[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = i0 + u * (int64_t)blockDim.x;
+                if (i < e) {
+                    fp16[i] = (uint16_t)p[u];
+                    rec[i] = (uint64_t)((uint32_t)g[u] * P + (uint32_t)p[u]) | ((uint64_t)t << kb) |
+                             ((uint64_t)(i - s) << (kb + 18));
+                }
+            }
         }
     }
 }
@@ -503,7 +615,15 @@ __global__ __launch_bounds__(256) void k_gkeys_pm(const int64_t* __restrict__ G_
         const int64_t b = G_off[L], e = G_off[L + 1];
         const int64_t o = (int64_t)pm_off[(int64_t)p * n_ids + g];
         const uint64_t pg = ((uint64_t)p << 18) | ((uint64_t)g << 30);
-        for (int64_t k = b + lane; k < e; k += 64) rec[o + (k - b)] = (uint64_t)(uint32_t)G_tet[k] | pg;
+        // four 64-entry chunks per round, loads first (clamped, not branched)
+        for (int64_t k0 = b + lane; k0 < e; k0 += 4 * 64) {
+            uint32_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = (uint32_t)G_tet[min(k0 + u * 64, e - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u * 64 < e) rec[o + (k0 + u * 64 - b)] = (uint64_t)t[u] | pg;
+        }
     }
 }
 
