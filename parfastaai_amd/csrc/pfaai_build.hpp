@@ -139,39 +139,4 @@ __global__ __launch_bounds__(256) void k_g_check(const int64_t* __restrict__ Lp,
     }
 }
 
-// G_end[k] = the end of the F run (t, p) of G entry k of list (g, p): the
-// run-end table (k_blk_end, u32, p-major) looked up once per load.  One wave
-// per list, the lists taken protein-major (all genomes of protein p, then
-// p + 1): the waves in flight at any time look up one or two protein rows
-// of the table (640 KB each), which stay in every XCD's L2 -- genome-major
-// order touched all 100 rows at once (4.5 ms at 10k, mostly L2 misses).
-__global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
-                                              int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
-                                              uint32_t* __restrict__ G_end) {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t n_ids = n_lists / P;
-    for (int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < n_lists; q += waves) {
-        const int64_t p = q / n_ids, L = (q - p * n_ids) * P + p;
-        const int64_t row = p * kNTetramers;
-        const int64_t b = G_off[L], e = G_off[L + 1];
-        // four 64-entry chunks per round: every G_tet load, then every table
-        // lookup, then the stores (a list is ~290 entries at 10k: two rounds
-        // of two dependent loads instead of five)
-        // (indices clamped into the list rather than loads under a branch,
-        // which the compiler waits for at the branch)
-        for (int64_t k0 = b + lane; k0 < e; k0 += 4 * 64) {
-            int32_t t[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] = G_tet[min(k0 + u * 64, e - 1)];
-            uint32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = ends[row + t[u]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (k0 + u * 64 < e) G_end[k0 + u * 64] = v[u];
-        }
-    }
-}
-
 }  // namespace pfaai

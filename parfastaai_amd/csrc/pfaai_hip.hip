@@ -470,7 +470,7 @@ int ensure_tsort(pfaai_ctx* c, int64_t n, int kb, bool keygen) {
     int rc;
     if ((rc = ensure(c, c->srec_a, nn * 8)) || ((keygen || passes > 2) && (rc = ensure(c, c->srec_b, nn * 8))) ||
         (rc = ensure(c, c->shist, (size_t)ntiles * (4u << db))) ||
-        (rc = ensure(c, c->sgsum, (size_t)ngroups * (4u << db))) || (rc = ensure(c, c->sbase, 4u << db)))
+        (rc = ensure(c, c->sgsum, (size_t)ngroups * (4u << db))) || (rc = ensure(c, c->sbase, (4u << db) + 64)))
         return rc;
     return PFAAI_RC_OK;
 }
@@ -486,6 +486,7 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
     auto* hist = static_cast<uint32_t*>(c->shist.p);
     auto* gsum = static_cast<uint32_t*>(c->sgsum.p);
     auto* base = static_cast<uint32_t*>(c->sbase.p);
+    uint32_t* tctr = base + (1 << DB);  // the scatter's per-XCD tile counters (zeroed by k_sort_top)
     uint64_t* buf[2] = {static_cast<uint64_t*>(c->srec_a.p), static_cast<uint64_t*>(c->srec_b.p)};
     const size_t lds = sort_scatter_lds<DB, NT>();
     // persistent scatter: as many workgroups as fit the CUs (two 512-thread
@@ -508,10 +509,10 @@ void tsort_launch(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int k
             hipLaunchKernelGGL((k_sort_hist<DB, NT, SrcRecs>), dim3(ntiles), dim3(NT), 0, s, prev, n, shift, mask,
                                hist);
         hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
-        hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base);
+        hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base, tctr);
 #define SC(SRC_T, SRC, DST_T, DST)                                                                        \
     hipLaunchKernelGGL((k_sort_scatter<DB, NT, PF, SRC_T, DST_T, VAR>), dim3(grid), dim3(NT), lds, s, SRC, DST, n, ntiles, \
-                       shift, mask, hist, gsum, base)
+                       shift, mask, hist, gsum, base, tctr)
         if (pass == 0 && last) SC(S0, src0, DN, dstN);
         else if (pass == 0) SC(S0, src0, DstRecs, next);
         else if (last) SC(SrcRecs, prev, DN, dstN);
@@ -538,15 +539,19 @@ int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipSt
     // next-tile prefetch), PFAAI_TSORT_PF=0|1 the prefetch of the 512 form
     const char* nt = DIAG_ENV("PFAAI_TSORT_NT");
     const char* pf = DIAG_ENV("PFAAI_TSORT_PF");
-    if (const char* vr = DIAG_ENV("PFAAI_TSORT_VAR"); vr && db == 10) {  // scatter variants / ablations (A/B)
-        switch (atoi(vr)) {
-            case 1: tsort_launch<10, kSortNT, kSortPF, S0, DN, 1>(c, src0, dstN, n, kb, passes, s); break;
-            case 3: tsort_launch<10, kSortNT, kSortPF, S0, DN, 3>(c, src0, dstN, n, kb, passes, s); break;
-            case 5: tsort_launch<10, kSortNT, kSortPF, S0, DN, 5>(c, src0, dstN, n, kb, passes, s); break;
-            case 9: tsort_launch<10, kSortNT, kSortPF, S0, DN, 9>(c, src0, dstN, n, kb, passes, s); break;
-            case 13: tsort_launch<10, kSortNT, kSortPF, S0, DN, 13>(c, src0, dstN, n, kb, passes, s); break;
-            default: tsort_launch<10, kSortNT, kSortPF, S0, DN, 0>(c, src0, dstN, n, kb, passes, s); break;
-        }
+    if (const char* vr = DIAG_ENV("PFAAI_TSORT_VAR"); vr && (db == 10 || db == 8)) {  // scatter variants / ablations (A/B)
+#define TV(D, V) tsort_launch<D, kSortNT, kSortPF, S0, DN, V>(c, src0, dstN, n, kb, passes, s)
+#define TVS(D)                                    \
+    switch (atoi(vr)) {                           \
+        case 1: TV(D, 1); break;                  \
+        case 16: TV(D, 16); break;                \
+        case 32: TV(D, 32); break;                \
+        case 48: TV(D, 48); break;                \
+        default: TV(D, 0); break;                 \
+    }
+        if (db == 8) { TVS(8) } else { TVS(10) }
+#undef TVS
+#undef TV
         HIPCHK(c, hipGetLastError());
         return PFAAI_RC_OK;
     }
@@ -612,37 +617,31 @@ int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool wa
 
 // Both F and G given with |G| = |F|: G must be F's genome-major transpose.
 // One two-pass sort of F by (genome, protein) -- records (key, F index),
-// read straight from F -- yields G_pos and checks the caller's list bounds
-// per entry and its tetramers by the keyed pair-hash sums (DstGposHash,
-// k_hash_f).  Returns -1 on a mismatch.
-int check_g_transpose(pfaai_ctx* c, int64_t ng, int64_t n_f, bool want_pos, hipStream_t s) {
-    const int kb = bits_for(ng);
+// read straight from F -- yields G_pos (into gpos) and the sort side of the
+// list-bound sum (DstGposHash); k_hash_f the F side of the tetramer sum.  The
+// G sides come from k_gend (HASH), launched by load_impl, which then compares
+// all four (finish_g_check).
+int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, hipStream_t s) {
+    const int kb = bits_for((int64_t)c->prob.n_ids * c->prob.n_prot);
     int rc;
     if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
-    // G_pos is the sort's output even when the row kernels will not use it
-    // (a scratch buffer then)
-    if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;  // (released with the sort space)
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    int* err = reinterpret_cast<int*>(sc + SC_ERR);
-    auto* sums = sc + SC_HG;  // [0]: over G, [1]: over F (SC_HF)
-    HIPCHK(c, hipMemsetAsync(err, 0, sizeof(int), s));
-    HIPCHK(c, hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), s));
-    const uint64_t seed = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
-                          (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    HIPCHK(c, hipMemsetAsync(sc + SC_HG, 0, 4 * sizeof(unsigned long long), s));  // SC_HG, SC_HF, SC_HL, SC_HT
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
-    const DstGposHash dst{static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->rec_c.p),
-                          static_cast<const int32_t*>(c->G_tet.p), static_cast<const int64_t*>(c->G_off.p), seed, err,
-                          sums};
+    const DstGposHash dst{gpos, seed, sc + SC_HG};
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
-    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p), seed, sums + 1);
+    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p), seed, sc + SC_HF);
     HIPCHK(c, hipGetLastError());
-    int bad = 0;
-    unsigned long long h[2] = {0, 0};
-    HIPCHK(c, hipMemcpyAsync(&bad, err, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(h, sums, sizeof(h), hipMemcpyDeviceToHost, s));
+    return PFAAI_RC_OK;
+}
+
+// After k_gend<*, true>: -1 unless both sum pairs agree.
+int finish_g_check(pfaai_ctx* c, hipStream_t s) {
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIPCHK(c, hipMemcpyAsync(h, static_cast<unsigned long long*>(c->scalars.p) + SC_HG, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    return (bad || h[0] != h[1]) ? -1 : PFAAI_RC_OK;
+    return (h[0] != h[2] || h[1] != h[3]) ? -1 : PFAAI_RC_OK;  // [HG, HF, HL, HT]
 }
 
 // G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
@@ -953,14 +952,19 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         }
     }
     bool has_g = in_g;
+    uint32_t* gpos_chk = nullptr;  // both given: the sort's G_pos, whose sums k_gend completes
+    uint64_t check_seed = 0;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
         // the transpose of F -- one sort of F by (genome, protein) proves it
         // against the caller's lists (and yields G_pos): no search per entry
-        rc = check_g_transpose(c, ng, n_f, want_pos, s);
-        if (rc == -1)
-            return fail(c, PFAAI_RC_INVALID, "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
-        if (rc) return rc;
+        // (G_pos is the sort's output even when the row kernels will not use
+        // it: a scratch buffer then, released with the sort space)
+        if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;
+        gpos_chk = static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->rec_c.p);
+        check_seed = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
+                     (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        if ((rc = check_g_transpose(c, n_f, gpos_chk, check_seed, s))) return rc;
         pos_ok = fp16_done = true;
         c->load_path = PFAAI_LOAD_G_CHECKED;
     } else if (in_g && in_f && n_f) {  // both given, G larger (QT: both DBs' lists): G must hold F (k_g_check)
@@ -1053,16 +1057,37 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     // no run table.
     d.G_end = nullptr;
     c->runs_valid = false;
-    if (d.G_pos) {
-        if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
-        if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
-        hipLaunchKernelGGL(k_gend, dim3((int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, 4), 1), 1 << 16)), dim3(256),
-                           0, s, d.G_off, d.G_tet, ng, P, reinterpret_cast<const uint32_t*>(c->blk.p),
-                           static_cast<uint32_t*>(c->G_end.p));
-        HIPCHK(c, hipGetLastError());
-        d.G_end = static_cast<const uint32_t*>(c->G_end.p);
-    } else {
-        release(c->G_end);
+    {
+        // k_gend: G_end (with G_pos) and / or the G sides of the both-given check
+        const int ggrid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, kGendLists), 1), 1 << 16);
+        auto* sums = static_cast<unsigned long long*>(c->scalars.p) + SC_HL;
+        if (d.G_pos) {
+            if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
+            if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
+            const auto* ends = reinterpret_cast<const uint32_t*>(c->blk.p);
+            auto* gend = static_cast<uint32_t*>(c->G_end.p);
+            if (gpos_chk)
+                hipLaunchKernelGGL((k_gend<true, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
+                                   gend, gpos_chk, check_seed, sums);
+            else
+                hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
+                                   gend, nullptr, 0ull, nullptr);
+            HIPCHK(c, hipGetLastError());
+            d.G_end = static_cast<const uint32_t*>(c->G_end.p);
+        } else {
+            release(c->G_end);
+            if (gpos_chk) {
+                hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
+                                   nullptr, nullptr, gpos_chk, check_seed, sums);
+                HIPCHK(c, hipGetLastError());
+            }
+        }
+        if (gpos_chk && (rc = finish_g_check(c, s))) {
+            if (rc == -1)
+                return fail(c, PFAAI_RC_INVALID,
+                            "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");
+            return rc;
+        }
     }
     HIPCHK(c, hipEventRecord(c->load_ev[1], s));
 

@@ -70,6 +70,10 @@ struct SrcFKeys {
     __device__ __forceinline__ uint64_t load(int64_t i) const {
         return (uint64_t)((uint32_t)Fg[i] * P + (uint32_t)Fp[i]) | ((uint64_t)i << 32);
     }
+    __device__ __forceinline__ uint64_t load_nt(int64_t i) const {  // streamed once: no L2 residency wanted
+        return (uint64_t)((uint32_t)__builtin_nontemporal_load(Fg + i) * P + (uint32_t)__builtin_nontemporal_load(Fp + i)) |
+               ((uint64_t)i << 32);
+    }
 };
 
 // materialised records (later passes; first passes of the keygen paths)
@@ -77,6 +81,7 @@ struct SrcRecs {
     const uint64_t* r;
     __device__ __forceinline__ uint64_t hist_rec(int64_t i, bool) const { return r[i]; }
     __device__ __forceinline__ uint64_t load(int64_t i) const { return r[i]; }
+    __device__ __forceinline__ uint64_t load_nt(int64_t i) const { return __builtin_nontemporal_load(r + i); }
 };
 
 // ---- destinations (last pass) ----------------------------------------------
@@ -98,18 +103,21 @@ struct DstRecs {
 
 // Both F and G given (records key g * P + p | F index << 32, sorted = F's
 // genome-major transpose): G_pos[pos] = F index i, and the caller's G must BE
-// that transpose --
-//   list bounds: its list (g, p) must span pos (G_off[key] <= pos <
-//     G_off[key + 1]; with |G| = |F| and G_off monotone that pins every
-//     list bound); a mismatch sets *err;
-//   tetramers: its tetramer at pos must be F entry i's.  F entry i's tetramer
-//     is not in the record (key 21 + tetramer 18 + index 30 bits do not fit
-//     64), so the check is a keyed hash of the pairs: the sum over G of
-//     h(G_pos[k], G_tet[k]) (here, from coalesced reads) must equal the sum
-//     over F of h(i, t(i)) (k_hash_f, from Lp alone).  G_pos is a bijection
-//     onto F by construction, so the sums differ unless every tetramer
-//     matches, except with probability ~2^-64 (h is a 64-bit mix of the
-//     injective (i, t) code, keyed by a per-load random seed).
+// that transpose.  Both halves of that are proven by keyed hash sums, so the
+// write phase loads nothing (the first form read G_off[key], G_off[key + 1]
+// and G_tet[pos] for every record: ~3 random L2 requests per record, 3.4 ms
+// of a 10k load's pass):
+//   list bounds: the sum over sorted positions of hp(pos, key) (here) must
+//     equal the sum over G's lists of hp(pos, list) for every position of
+//     every list (k_gend) -- the key sequence the sort produced is then the
+//     one G_off describes;
+//   tetramers: the sum over G of h(G_pos[k], G_tet[k]) (k_gend) must equal
+//     the sum over F of h(i, t(i)) (k_hash_f, from Lp alone).  G_pos is a
+//     bijection onto F by construction, so the sums differ unless every
+//     tetramer matches.
+// Either sum pair agrees for different inputs with probability ~2^-64 (h
+// and hp are a 64-bit mix of an injective code, keyed by a per-load random
+// seed).
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser (a bijection)
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -117,31 +125,23 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
     return x ^ (x >> 31);
 }
 __device__ __forceinline__ uint64_t pair_hash(uint64_t seed, uint64_t i, uint32_t t) {
-    return mix64(seed ^ ((i << 18) | t));  // i < 2^32, t < 2^18: an injective 50-bit code
+    return mix64(seed ^ ((i << 18) | t));  // i < 2^32, t < 2^18 (host-checked): an injective 50-bit code
+}
+__device__ __forceinline__ uint64_t pos_hash(uint64_t seed, uint32_t pos, uint32_t key) {
+    return mix64(~seed ^ (((uint64_t)pos << 32) | key));
 }
 
 struct DstGposHash {
     uint32_t* G_pos;
-    const int32_t* G_tet;
-    const int64_t* G_off;
     uint64_t seed;
-    int* err;
     unsigned long long* sum;
     static constexpr int kWH = kSortItems;
     static constexpr bool kSum = true;
-    struct Aux {
-        uint32_t lo, hi;  // list bounds (< 2^32: |G| = |F| <= 2^32 - 64)
-        int32_t tu;
-    };
-    __device__ __forceinline__ Aux fetch(int64_t pos, uint64_t v) const {
-        const uint32_t key = (uint32_t)v;
-        return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_tet[pos]};
-    }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
-        const uint32_t i = (uint32_t)(v >> 32);
-        G_pos[pos] = i;
-        if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
-        return pair_hash(seed, i, (uint32_t)a.tu & 0x3FFFFu) + (uint64_t)((uint32_t)a.tu >> 18);  // (t >= 2^18: never equal)
+    struct Aux {};
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
+        G_pos[pos] = (uint32_t)(v >> 32);
+        return pos_hash(seed, (uint32_t)pos, (uint32_t)v);
     }
 };
 
@@ -278,7 +278,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_grp(uint32_t* __restrict_
 // exclusive prefix of the bin totals
 template <int DB>
 __global__ __launch_bounds__(kSortThreads) void k_sort_top(uint32_t* __restrict__ gsum, int64_t ngroups,
-                                                           uint32_t* __restrict__ binbase) {
+                                                           uint32_t* __restrict__ binbase, uint32_t* __restrict__ tctr) {
+    if (threadIdx.x < 8) tctr[threadIdx.x] = 0u;  // the scatter's per-XCD tile counters
     constexpr int BINS = 1 << DB;
     constexpr int BPT = BINS > kSortThreads ? BINS / kSortThreads : 1;  // bins per thread
     __shared__ uint32_t wsum[kSortThreads / 64];
@@ -345,13 +346,13 @@ constexpr int sort_scatter_wpe() { return NT == 512 ? 4 : 1; }
 // PF: the next tile's records and digit bases are loaded while this tile is
 // ranked and written (16 + BPT VGPRs live across the tile)
 // VAR (diagnostics A/B, 0 in the product): bit 0 round-robin tile order,
-// bit 1 the ranking ballots done twice (their cost), bit 2 records stored straight
-// from registers at their ranked positions (no LDS reorder), bit 3 no global
-// stores (ablation)
+// bit 1 the ranking ballots done twice (their cost), bit 3 no global stores
+// (ablation), bit 4 ordinary (temporal) record loads, bit 5 a static tile
+// stride instead of the per-XCD tile counters (tctr[8], zeroed by k_sort_top)
 template <int DB, int NT, bool PF, class Src, class Dst, int VAR = 0>
 __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
     Src src, Dst dst, int64_t n, int64_t ntiles, int shift, uint32_t mask, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ gsum, const uint32_t* __restrict__ binbase) {
+    const uint32_t* __restrict__ gsum, const uint32_t* __restrict__ binbase, uint32_t* __restrict__ tctr) {
     constexpr int BINS = 1 << DB, W = NT / 64, kTile = sort_tile<NT>();
     constexpr int BPT = BINS > NT ? BINS / NT : 1;  // digits per thread (scans)
     // write phase: Dst::kWH records' destination loads issued before the
@@ -384,7 +385,10 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
             const int64_t i = t0 + (wid * kSortItems + k) * 64 + lane;
-            r[k] = src.load(i < n ? i : n - 1);
+            if constexpr ((VAR & 16) == 0)  // streamed once: non-temporal, the L2 keeps the output lines
+                r[k] = src.load_nt(i < n ? i : n - 1);
+            else
+                r[k] = src.load(i < n ? i : n - 1);
         }
         const int64_t grp = tc / kSortGroup;
 #pragma unroll
@@ -400,23 +404,42 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
     // every digit's output run, and whole lines leave its L2 (round-robin
     // tiles: 2.72 -> 2.32 ms for the 10k F -> G first pass); VAR bit 0 keeps
     // the round-robin order (A/B)
-    int64_t tile0 = blockIdx.x, tstep = gridDim.x, tend = ntiles;
+    int64_t tile0 = blockIdx.x, tstep = gridDim.x, tend = ntiles, xbase = 0;
+    const int xcd = blockIdx.x % 8;
+    bool dyn = false;
     if constexpr ((VAR & 1) == 0) {
-        const int64_t nx = gridDim.x / 8, x = blockIdx.x % 8;
+        const int64_t nx = gridDim.x / 8;
         if (nx >= 1 && (int64_t)gridDim.x % 8 == 0) {
             const int64_t per = (ntiles + 7) / 8;
-            tile0 = x * per + blockIdx.x / 8;
+            xbase = xcd * per;
+            tile0 = xbase + blockIdx.x / 8;
             tstep = nx;
-            tend = min(ntiles, (x + 1) * per);
+            tend = min(ntiles, (xcd + 1) * per);
+            dyn = (VAR & 32) == 0;
         }
     }
-    fetch_tile(tile0 < tend ? tile0 : ntiles, rec, gb);
-    for (int64_t tile = tile0; tile < tend; tile += tstep) {
+    __shared__ uint32_t s_next;
+    // the next tile: the XCD's next one, by one atomic per tile, so the
+    // tiles in flight on an XCD are consecutive and its L2 sees whole output
+    // lines (a static stride let fast workgroups run ahead: 2.33 -> 1.80 ms
+    // for the 10k F -> G first pass); VAR bit 5 keeps the static stride
+    auto next_tile = [&](int64_t cur) -> int64_t {
+        if (!dyn) return cur + tstep;
+        if (tid == 0) s_next = atomicAdd(&tctr[xcd], 1u);
+        __syncthreads();
+        return xbase + (int64_t)s_next;
+    };
+    int64_t tile = dyn ? next_tile(0) : tile0;
+    fetch_tile(tile < tend ? tile : ntiles, rec, gb);
+    while (tile < tend) {
         const int64_t t0 = tile * kTile;
-        const int64_t tnext = tile + tstep < tend ? tile + tstep : ntiles;
+        int64_t tnext = 0;
         uint64_t nrec[kSortItems];
         uint32_t ngb[BPT];
-        if constexpr (PF) fetch_tile(tnext, nrec, ngb);  // in flight during this tile
+        if constexpr (PF) {  // in flight during this tile
+            tnext = next_tile(tile);
+            fetch_tile(tnext < tend ? tnext : ntiles, nrec, ngb);
+        }
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
             const int b = tid + q * NT;
@@ -490,27 +513,6 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             off += tot[q];
         }
         __syncthreads();
-        if constexpr ((VAR & 4) != 0) {  // straight from registers: position gbase + wave prefix + rank
-#pragma unroll
-            for (int k = 0; k < kSortItems; ++k) {
-                if (t0 + (wid * kSortItems + k) * 64 + lane < n) {
-                    const uint32_t d = sort_digit(rec[k], shift, mask);
-                    const uint32_t pos = gbase[d] + cnt[wid * BINS + d] + lr[k];
-                    const auto ax = dst.fetch(pos, rec[k]);
-                    if constexpr ((VAR & 8) == 0) hsum += dst.store(pos, rec[k], ax);
-                }
-            }
-            __syncthreads();
-            if constexpr (PF) {
-#pragma unroll
-                for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
-#pragma unroll
-                for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
-            } else {
-                fetch_tile(tnext, rec, gb);
-            }
-            continue;
-        }
         {
             uint32_t slot[kSortItems];  // every LDS read issued before the first write
 #pragma unroll
@@ -558,8 +560,10 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
 #pragma unroll
             for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
         } else {
-            fetch_tile(tnext, rec, gb);
+            tnext = next_tile(tile);
+            fetch_tile(tnext < tend ? tnext : ntiles, rec, gb);
         }
+        tile = tnext;
     }
     if constexpr (Dst::kSum) {
 #pragma unroll
@@ -643,6 +647,109 @@ __global__ void k_len_from_t(const int32_t* __restrict__ T, int32_t P, int32_t n
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = k / P, p = k % P;
         len[k] = (uint32_t)T[p * t_cols + g];
+    }
+}
+
+// k_gend over G, list by list (one pass over G_tet, G_pos):
+//   END:  G_end[k] = the end of the F run (t, p) of G entry k of list (g, p),
+//         from the run-end table (k_blk_end, u32, p-major) -- looked up once
+//         per load, so the WK 3 row kernel reads (G_pos, G_end) coalesced;
+//   HASH: the G sides of the both-given check (DstGposHash): sums[0] +=
+//         hp(k, list of k), sums[1] += h(G_pos[k], G_tet[k]).
+// The lists are taken protein-major (all genomes of protein p, then p + 1),
+// so the table lookups in flight hit one or two protein rows (640 KB each),
+// which stay in every XCD's L2 -- genome-major order touched all 100 rows at
+// once (4.5 ms at 10k, mostly L2 misses).  A workgroup takes kGendLists
+// consecutive lists and walks their entries as one flat range, four entries
+// per thread in flight.  (The lookups are random 4-B requests: one L2 request
+// per entry bounds it, ~1.8 ms at 10k.)
+constexpr int kGendLists = 32;
+
+template <bool END, bool HASH>
+__global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
+                                              int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
+                                              uint32_t* __restrict__ G_end, const uint32_t* __restrict__ G_pos,
+                                              uint64_t seed, unsigned long long* __restrict__ sums) {
+    __shared__ int64_t lb[kGendLists];
+    __shared__ uint32_t pre[kGendLists + 1];
+    __shared__ int64_t row[kGendLists];
+    __shared__ uint32_t lid[kGendLists];
+    const int tid = threadIdx.x;
+    const int64_t n_ids = n_lists / P;
+    uint64_t hl = 0, ht = 0;
+    for (int64_t q0 = (int64_t)blockIdx.x * kGendLists; q0 < n_lists; q0 += (int64_t)gridDim.x * kGendLists) {
+        if (tid < 64) {  // one wave: the block's lists, their lengths and an inclusive scan
+            uint32_t len = 0;
+            if (tid < kGendLists) {
+                const int64_t q = min(q0 + tid, n_lists - 1);
+                const int64_t p = q / n_ids, L = (q - p * n_ids) * P + p;
+                const int64_t b = G_off[L], e = G_off[L + 1];
+                lb[tid] = b;
+                row[tid] = p * kNTetramers;
+                lid[tid] = (uint32_t)L;
+                len = q0 + tid < n_lists ? (uint32_t)(e - b) : 0u;
+            }
+            uint32_t inc = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(inc, o, 64);
+                if (tid >= o) inc += u;
+            }
+            if (tid < kGendLists) pre[tid + 1] = inc;
+            if (tid == 0) pre[0] = 0u;
+        }
+        __syncthreads();
+        const uint32_t total = pre[kGendLists];
+        for (uint32_t f0 = tid; f0 < total; f0 += 4 * 256) {
+            int64_t k[4];
+            int64_t rw[4];
+            uint32_t li[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t f = min(f0 + (uint32_t)u * 256u, total - 1u);
+                int lo = 0;  // the list j with pre[j] <= f < pre[j + 1]
+#pragma unroll
+                for (int w = kGendLists / 2; w > 0; w >>= 1)
+                    if (pre[lo + w] <= f) lo += w;
+                k[u] = lb[lo] + (f - pre[lo]);
+                rw[u] = row[lo];
+                li[u] = lid[lo];
+            }
+            int32_t t[4];
+            uint32_t gp[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // (streamed once: non-temporal, the L2 keeps the table rows)
+                t[u] = __builtin_nontemporal_load(G_tet + k[u]);
+                if constexpr (HASH) gp[u] = __builtin_nontemporal_load(G_pos + k[u]);
+            }
+            uint32_t v[4];
+            if constexpr (END) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = ends[rw[u] + t[u]];  // (G_tet < 160000: host-checked)
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (f0 + (uint32_t)u * 256u < total) {
+                    if constexpr (END) G_end[k[u]] = v[u];
+                    if constexpr (HASH) {
+                        hl += pos_hash(seed, (uint32_t)k[u], li[u]);
+                        ht += pair_hash(seed, gp[u], (uint32_t)t[u]);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // lb / pre / row / lid are rewritten by the next block
+    }
+    if constexpr (HASH) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            hl += __shfl_down(hl, o, 64);
+            ht += __shfl_down(ht, o, 64);
+        }
+        if ((tid & 63) == 0) {
+            atomicAdd(&sums[0], (unsigned long long)hl);
+            atomicAdd(&sums[1], (unsigned long long)ht);
+        }
     }
 }
 

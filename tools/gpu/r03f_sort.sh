@@ -22,7 +22,7 @@ tail -2 $OUT/pytest.log
 IFS="|" read -ra VLIST <<< "${VARIANTS:-nt1024 PFAAI_TSORT_NT=1024|pf1 PFAAI_TSORT_PF=1|pf0 PFAAI_TSORT_PF=0}"
 for v in "${VLIST[@]}"; do
   set -- $v
-  tag=$1; envv=$2
+  tag=$1; shift; envv="$*"
   for orient in ${ORIENTS:-both g f}; do
     env PFAAI_HIP_LIB=$LIB $envv timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$PWD/$OUT/${tag}_$orient" -o run -- python3 tools/gpu/load_bench.py --orient $orient --reps 2 \
