@@ -504,11 +504,18 @@ def main():
         # the two-pass sort moves ~50 B (pfaai_sort.hpp: per pass a histogram
         # read + a read and a write of 8-B records)
         alg_per_f = {"g_checked": 22, "g_from_f": 26, "f_from_g": 22}.get(load_path)
+        # the bytes the implemented passes move per F entry (G_CHECKED): hist 1
+        # reads F 8 + writes the u16 column 2; scatter 1 reads 8, writes 8;
+        # hist 2 reads 8; scatter 2 reads 8, writes G_pos 4; k_gend reads
+        # G_tet 4 + G_pos 4 + a 4-B run end, writes G_end 4 = 62 B
+        pass_per_f = {"g_checked": 62}.get(load_path)
         load = {"path": load_path, "device_ms": round(ms_load_dev, 3), "host_checks_ms": round(ms_checks, 1),
                 "h2d_ms": round(ms_upload, 1), "wall_ms": round(load_wall_ms, 1), "F": n_f,
                 "alg_bytes_per_F": alg_per_f,
                 "alg_GBps": round(alg_per_f * n_f / (ms_load_dev * 1e-3) / 1e9, 1) if alg_per_f else None,
                 "frac": round(alg_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if alg_per_f else None,
+                "pass_bytes_per_F": pass_per_f,
+                "pass_frac": round(pass_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pass_per_f else None,
                 "one_shot_ms": round(ms_load_dev + first_step_ms, 3), "first_step_ms": round(first_step_ms, 3),
                 "one_shot_wall_ms": round(first_wall_ms, 1)}
         cpu = None

@@ -11,6 +11,19 @@
 
 namespace pfaai_impl {
 
+// k_rows_pl's lookahead form (LA): measured no faster on the narrow
+// launches it fits (8-way shards at 10k: last shard 1.08 -> 1.10 ms, stage
+// clocks in profiles/r03n_*: the per-protein chain of a narrow row is the
+// busy waves' instruction stream, not the member-load latency LA hides), so
+// the product does not take it; the diagnostics build keeps it for A/B
+// (PFAAI_PL_LAKW=<max KW>, PFAAI_PL_CLK_LA=1 for its stage clocks)
+constexpr int kLaKwMax = 0;
+#ifdef PFAAI_DIAGNOSTICS
+constexpr int kLaKwInst = 5;  // (KW 4 / 5 spill)
+#else
+constexpr int kLaKwInst = 0;
+#endif
+
 template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = true, int VAR = 0>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
@@ -29,14 +42,37 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     // all-vs-all rows in one chunk with G_pos loaded: each run walk starts just
     // past the row genome (k_rows_pl WK 3, pl_issue_m2<A8>)
     const bool gp = MODE == 0 && wk == 1 && pl_uses_ends(c, MODE);
+    // the lookahead form (member loads one protein ahead, k_rows_pl LA) where
+    // its registers fit: KW <= kLaKwMax (PFAAI_PL_LAKW=0..5 in diagnostics, A/B)
+    int la_kw = kLaKwMax;
+    if (const char* v = DIAG_ENV("PFAAI_PL_LAKW")) la_kw = atoi(v);
+    const bool la = gp && NK == 1 && NT == 1024 && KW <= la_kw;
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #define PLK(BF, WKV)                                                                                                 \
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, WKV>), dim3(r1 - r0, gy), dim3(NT), lds, \
                        s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+#define PLKA(BF)                                                                                                     \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, 3, true>), dim3(r1 - r0, gy), dim3(NT), \
+                       lds, s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
         if (wk == 0 || abs_chunk >= 0) {
             if (bigf) PLK(true, 0); else PLK(false, 0);
         } else if constexpr (kWk1 != 0) {
             if constexpr (MODE == 0) {
+                if constexpr (NK == 1 && NT == 1024 && KW <= kLaKwInst) {
+                    if (la) {
+#ifdef PFAAI_DIAGNOSTICS
+                        if (!bigf && DIAG_ENV("PFAAI_PL_CLK_LA") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {  // stage clocks (the G_pos path stays on: not PFAAI_PL_CLK)
+                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, true, BR, VAR, 3, true>),
+                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, abs_chunk, flags,
+                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
+                                               static_cast<unsigned long long*>(c->dbg.p));
+                            return;
+                        }
+#endif
+                        if (bigf) PLKA(true); else PLKA(false);
+                        return;
+                    }
+                }
                 if (gp) {
                     if (bigf) PLK(true, 3); else PLK(false, 3);
                     return;
@@ -45,6 +81,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
             if (bigf) PLK(true, kWk1); else PLK(false, kWk1);
         }
 #undef PLK
+#undef PLKA
     };
     if (nchunks == 1 || !c->windows) {
         rows(c->dev, rb, re, nchunks, -1);
@@ -191,6 +228,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "g4") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "noskip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "n16") { launch_pl<MODE, 5, 1024, 8, 1, true, 1024>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "s1skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 128>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

@@ -207,8 +207,16 @@ constexpr int kClkBlocks = 256;
 // vector loads in order, so an S5 after the prefetches waited for the
 // members and run-table entries just issued (s_waitcnt vmcnt(0)) -- first, it
 // waits only for loads of the previous iteration, needed by now anyway.
+// LA (lookahead, WK 3 with N in LDS only): the first round of a protein's
+// member loads is issued at the end of the PREVIOUS iteration and stays in
+// flight across the barrier, S5 and S3 -- the per-protein chain no longer
+// waits for member lines once per protein.  Its tasks must then be cut two
+// proteins ahead (S3(i+2), S2(i+3), S1(i+4)), so the task / run slots are
+// three (q % 3) and the task counter sets four (q % 4).  It needs the 9
+// VGPRs of the loads in flight across the barrier: the narrow launches (KW
+// <= 2) have them within the 64-VGPR budget.
 template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, int NK = 0, bool BIGF = false,
-          bool S5F = true, bool BR = false, int VAR = 0, int WK = 0>
+          bool S5F = true, bool BR = false, int VAR = 0, int WK = 0, bool LA = false>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
                                                    uint32_t flags,
                                                    const unsigned long long* __restrict__ first_key,
@@ -222,11 +230,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr bool NL = NK == 1;
     constexpr int NN = NK == 0 ? KW : NK == 2 ? (KW + 1) / 2 : 1;  // N registers
     constexpr int TC = NL ? kPlTaskCap / 2 : kPlTaskCap;  // line tasks per stage
+    static_assert(!LA || (WK == 3 && NK == 1 && S5F), "the lookahead form is WK 3 with N in LDS");
+    constexpr int NSL = LA ? 3 : 2;                      // task / run slots (protein % NSL)
+    constexpr int NCS = LA ? 4 : 3;                      // task counter sets (protein % NCS)
     extern __shared__ uint32_t pl_smem[];                // acc[2][W], goff[P + 1], (NL) n16[W]
-    __shared__ uint2 rt[2][kPlEntries];                  // runs of a protein stage: member range [lo, hi)
-    __shared__ uint16_t tk[2][TC];                       // line tasks
-    __shared__ uint32_t wmask[3][kPlEntries / 32];       // whole-workgroup runs, by protein % 3
-    __shared__ uint32_t ntask[3], nwhole[3];             // by protein % 3
+    __shared__ uint2 rt[NSL][kPlEntries];                // runs of a protein stage: member range [lo, hi)
+    __shared__ uint16_t tk[NSL][TC];                     // line tasks
+    __shared__ uint32_t wmask[NCS][kPlEntries / 32];     // whole-workgroup runs, by protein % NCS
+    __shared__ uint32_t ntask[NCS], nwhole[NCS];         // by protein % NCS
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int grp = tid >> 2, gl = tid & 3;
@@ -264,8 +275,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     for (int w = tid; w < 2 * W; w += NT) acc[w] = 0u;
     if (NL)
         for (int w = tid; w < NWORDS; w += NT) n32[w] = 0u;
-    if (tid < 3) { ntask[tid] = 0u; nwhole[tid] = 0u; }
-    for (int w = tid; w < 3 * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
+    if (tid < NCS) { ntask[tid] = 0u; nwhole[tid] = 0u; }
+    for (int w = tid; w < NCS * (kPlEntries / 32); w += NT) (&wmask[0][0])[w] = 0u;
     const int32_t tca = compat ? d.tcol_row[a] : a;  // T column of genomeA (row Q quirk only in compat)
     for (int p = tid; p < P; p += NT) taL[p] = (uint16_t)d.T[(int64_t)p * d.t_cols + tca];
     const uint16_t* T16 = compat ? d.T16c : d.T16;
@@ -305,9 +316,16 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr bool GP = WK == 3;
     const rsrc_t r_gp = mk_rsrc(GP ? d.G_pos + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
     const rsrc_t r_ge = mk_rsrc(GP ? d.G_end + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
+    // WK 3: S1's loads are issued by every wave (out-of-range offsets read
+    // 0): a load issued under the wave skip made the number of loads in
+    // flight path-dependent, and the compiler then waited for everything
+    // (vmcnt(0)) wherever an older load was consumed -- the member loads in
+    // S4b waited for this iteration's G_pos / G_end loads (VAR bit 128 keeps
+    // the skip, A/B)
+    constexpr bool kSkipS1 = kSkip && !(GP && (VAR & 128) == 0);
     auto s1 = [&](int p, int32_t (&gt)[EPT], uint32_t (&gq)[EPT]) {  // G entries tid + j*NT of protein p (tetramer ids)
         const uint32_t o = p < P ? uni_u32(goff[p]) : 0u, n = glen(p);
-        if constexpr (kSkip) {
+        if constexpr (kSkipS1) {
             if (wbase0 >= n) return;
         }
 #pragma unroll
@@ -341,7 +359,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         }
     };
     auto s3 = [&](int q, const uint4 (&r4)[EPT], const uint32_t (&gq2)[EPT]) {  // line tasks of protein q
-        const int st = q & 1, cs = q % 3;
+        const int st = q % NSL, cs = q % NCS;
         if constexpr (kSkip) {
             if (wbase0 >= glen(q)) return;
         }
@@ -393,6 +411,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     };
 
     // prologue: tasks of protein 0; run-table entries of protein 1; G lists of protein 2
+    // (LA: tasks of proteins 0 and 1, entries of 2, lists of 3)
     int32_t gt[EPT];
     uint4 r4[EPT];
     uint32_t gq[EPT], gq2[EPT];
@@ -404,6 +423,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     s3(0, r4, gq2);
     s2(1, gt, r4, gq, gq2);
     s1(2, gt, gq);
+    if constexpr (LA) {
+        if (1 < P) s3(1, r4, gq2);
+        s2(2, gt, r4, gq, gq2);
+        s1(3, gt, gq);
+    }
     __syncthreads();
 
     unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -524,6 +548,69 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         pl_scatter4_m<MODE, WK>(d, a, bbh, m >> 4, acc_x - (cc0 >> 1), wlo, wspan);
     };
 
+    if constexpr (LA) {
+        // first round of protein 0's member loads, in flight into iteration 0
+        uint4 b, bh;
+        st_cur = 0;
+        uint32_t okm = issue2(grpx, glen(0) > 0u ? min((int)uni_u32(ntask[0]), TC) : 0, b, bh);
+#pragma unroll 1
+        for (int i = 0; i <= P; ++i) {
+            uint32_t* acc_i = acc + (i & 1) * W;
+            const bool has_i = i < P && glen(i) > 0u;
+            s5(i, twc, i >= 1 ? (int32_t)uni_u32(taL[i - 1]) : 0);
+            stamp(0);
+            if (i + 2 < P) s3(i + 2, r4, gq2);
+            stamp(1);
+            s2(i + 3, gt, r4, gq, gq2);
+            s1(i + 4, gt, gq);
+            stamp(2);
+            if (has_i) {
+                const int cs = i % NCS;
+                const int nt = min((int)uni_u32(ntask[cs]), TC);
+                scatter8(acc_i, b, bh, okm);  // the first round, loaded during the previous iteration
+                stamp(4);
+                st_cur = i % NSL;
+                for (int k = grpx + NGX; k < nt; k += NGX) {
+                    okm = issue2(k, nt, b, bh);
+                    scatter8(acc_i, b, bh, okm);
+                }
+                if (uni_u32(nwhole[cs])) {  // e.g. a tetramer shared by every genome
+                    for (int wd = 0; wd < kPlEntries / 32; ++wd) {
+                        uint32_t m = uni_u32(wmask[cs][wd]);
+                        while (m) {
+                            const int sb = __builtin_ctz(m);
+                            m &= m - 1u;
+                            const uint32_t rx = uni_u32(rt[st_cur][wd * 32 + sb].x), ry = uni_u32(rt[st_cur][wd * 32 + sb].y);
+                            for (uint32_t mm = rx + tid; mm < ry; mm += NT)
+                                pl_add<MODE>(d, a, d.Fg[mm], acc_i, cc0, wlo, whi);
+                        }
+                    }
+                }
+            }
+            stamp(5);
+            // T words of protein i for the next S5 (issued before the member
+            // loads below: S5 waits for them, not for the members)
+            {
+                const int pt = min(i, P - 1);
+                const uint32_t tso = (uint32_t)((int64_t)pt * t16w + (cc0 >> 1)) * 4u;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) twc[k] = bld_u32(r_t16, (uint32_t)tid * 4u, tso + (uint32_t)k * (NT * 4u));
+            }
+            // the first round of protein i + 1 (its tasks were cut in iteration i - 1)
+            {
+                const int q = i + 1;
+                const int ntq = (q < P && glen(q) > 0u) ? min((int)uni_u32(ntask[q % NCS]), TC) : 0;
+                st_cur = q % NSL;
+                okm = issue2(grpx, ntq, b, bh);
+            }
+            stamp(3);
+            // recycle the counter set of protein i + 3 (last read in iteration i - 1)
+            if (tid < kPlEntries / 32) wmask[(i + 3) % NCS][tid] = 0u;
+            if (tid == 32) { ntask[(i + 3) % NCS] = 0u; nwhole[(i + 3) % NCS] = 0u; }
+            __syncthreads();
+            stamp(6);
+        }
+    } else {
 #pragma unroll 1
     for (int i = 0; i <= P; ++i) {
         const int st = i & 1, cs = i % 3;
@@ -620,6 +707,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         __syncthreads();
         stamp(6);
     }
+    }  // !LA
     if constexpr (CLK) {
         if (lane == 0 && blockIdx.x < kClkBlocks && blockIdx.y == 0)
             for (int j = 0; j < 8; ++j) clk[((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 8 + j] = ck[j];

@@ -16,7 +16,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 world = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 g = syn.generate(n, 100)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
-eng = _capi.Engine(0)
+eng = _capi.Engine(0, lib_path=os.environ.get("PFAAI_HIP_LIB"))  # (the diagnostics library for A/B switches)
 eng.load(**ds.problem())
 rows, pairs = eng.shape()
 d = eng.alloc(pairs * 8)

@@ -23,6 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--genomes", type=int, default=10000)
 ap.add_argument("--v2", action="store_true")
 ap.add_argument("--rows", default=None, help="row range lo:hi (default: all rows)")
+ap.add_argument("--la", action="store_true", help="stage names of k_rows_pl's lookahead form (narrow launches)")
 a = ap.parse_args()
 g = syn.generate(a.genomes, 100)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
@@ -38,13 +39,16 @@ eng.timing(reset=True)
 eng.run(r0, r1, 0, d)
 _, _, r_plain = eng.timing(reset=True)
 eng.debug_clocks(arm=True)
-os.environ["PFAAI_V2_CLK" if a.v2 else "PFAAI_PL_CLK"] = "1"
+os.environ["PFAAI_V2_CLK" if a.v2 else "PFAAI_PL_CLK_LA" if a.la else "PFAAI_PL_CLK"] = "1"
 eng.run(r0, r1, 0, d)
 _, b, r = eng.timing(reset=True)
 c = eng.debug_clocks().astype(np.float64)
 if a.v2:
     names = ["T issue + S3", "M/S2/S1 issue", "S5 normalise", "S4 prefetched", "S4 further rounds", "long runs",
              "barrier"]
+elif a.la:
+    names = ["S5 normalise", "S3 tasks", "S2/S1 issue", "T + next round-1 issue", "S4b round 1 (prefetched)",
+             "S4b rounds 2+/whole", "recycle+barrier"]
 else:
     names = ["S4a issue", "S3 tasks", "S2/S1 issue", "-", "S4b round 1", "S4b rounds 2+/whole + T issue",
              "recycle+barrier", "S5 normalise (first)"]
