@@ -99,7 +99,7 @@ inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
         cut.push_back(n);
         return cut;
     }
-    const double k = 1.0 * (double)n;  // shard.FIXED_COST_FRACTION
+    const double k = 0.8 * (double)n;  // shard.FIXED_COST_FRACTION
     auto before = [&](int64_t a) { return (double)a * k + (double)a * n - (double)(a * (a + 1) / 2); };
     const double total = before(n);
     for (int r = 1; r < parts; ++r) {

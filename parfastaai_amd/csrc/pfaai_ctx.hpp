@@ -79,6 +79,7 @@ struct pfaai_ctx {
     DevBuf out_aji, out_S, out_N, dbg;
     DevBuf srec_a, srec_b, shist, sgsum, sbase;  // the load-time transposition sort (pfaai_sort.hpp)
     hipEvent_t load_ev[2] = {nullptr, nullptr};  // device span of the last load's F / G build
+    hipEvent_t side_ev[2] = {nullptr, nullptr};  // the load's fork to / join from copy_stream (k_hash_f)
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
     // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers

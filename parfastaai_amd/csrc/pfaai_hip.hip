@@ -630,9 +630,21 @@ int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, 
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
     const DstGposHash dst{gpos, seed, sc + SC_HG};
-    if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
-    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p), seed, sc + SC_HF);
+    // the F side of the tetramer sum needs only Lp: it runs on the second
+    // stream beside the sort (VALU work beside HBM-bound passes); the load's
+    // stream waits for it after the sort
+    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    hipEvent_t* ev = c->side_ev;
+    for (int k = 0; k < 2; ++k)
+        if (!ev[k]) HIPCHK(c, hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(ev[0], s));  // (after the sums were cleared)
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, ev[0], 0));
+    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->Lp.p), seed,
+                       sc + SC_HF);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(ev[1], c->copy_stream));
+    if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
+    HIPCHK(c, hipStreamWaitEvent(s, ev[1], 0));
     return PFAAI_RC_OK;
 }
 
@@ -935,6 +947,15 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     // transposition sorts on the way, else by k_fp16 below
     if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
     HIPCHK(c, hipMemsetAsync(c->Fp16.p, 0, (n_f + 16) * sizeof(uint16_t), s));
+    // the both-given path's device buffers, allocated before the device span
+    // starts (hipMalloc inside it left the stream idle: 8.5-9.0 ms measured
+    // for 7.8 ms of kernels at 10k)
+    if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
+        if ((rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
+        if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;
+        if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
+    }
     for (hipEvent_t& e : c->load_ev)
         if (!e) HIPCHK(c, hipEventCreate(&e));
     HIPCHK(c, hipEventRecord(c->load_ev[0], s));
@@ -1139,6 +1160,15 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
         return rc;
     }
     (void)hipMemset(c->scalars.p, 0, SC_N * sizeof(unsigned long long));
+    // the second stream (the load's k_hash_f beside the sort, the streamed
+    // outputs' copies) and the load's fork / join events: created here, since
+    // a stream's first creation costs milliseconds (a load that created it
+    // measured 13.6 ms of device span instead of 8.0 at 10k)
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
+    for (hipEvent_t& e : c->side_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    for (hipEvent_t& e : c->load_ev)
+        if (hipEventCreate(&e) != hipSuccess) e = nullptr;
     // every code object of the library loaded now rather than at the first
     // launch of one of its kernels (HIP's deferred loading), so no caller's
     // first run pays it (the CLI creates its first context on a thread during
@@ -1167,6 +1197,8 @@ int pfaai_destroy(pfaai_ctx* c) {
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->load_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->side_ev)
         if (e) (void)hipEventDestroy(e);
     release(c->st_dev);
     if (c->st_host) (void)hipHostFree(c->st_host);

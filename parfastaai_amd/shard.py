@@ -20,8 +20,11 @@ from __future__ import annotations
 # each launch takes the counter words its own widest row needs, narrow
 # shards got cheaper: 1.25 n -> 1.37, 1.0 n -> 1.29, 1.5 n -> 1.34
 # (profiles/r02m_shard_times_10k_x8.txt).  Balancing by pairs alone gives
-# the last rank (narrow rows) 2.5 ms.
-FIXED_COST_FRACTION = 1.0
+# the last rank (narrow rows) 2.5 ms.  Round 3's row kernel (G_end, no run
+# table in the step) moved the balance toward the wide rows: 1.0 n -> 1.22,
+# 0.9 n -> 1.16, 0.8 n -> 1.16, 0.7 n -> 1.15 ms (profiles/r03o/shard_times.txt;
+# the row-profile fit gives 0.92 n); 0.8 n sits in the middle of the flat part.
+FIXED_COST_FRACTION = 0.8
 
 
 def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: float | None = None):

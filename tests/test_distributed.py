@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from parfastaai_amd.shard import split_rows
+from parfastaai_amd.shard import FIXED_COST_FRACTION, split_rows
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -64,7 +64,7 @@ def test_split_rows_balanced():
         blocks = split_rows(n, w)
         assert blocks[0][0] == 0 and blocks[-1][1] == n
         assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
-        k = 1.0 * n  # shard.FIXED_COST_FRACTION
+        k = FIXED_COST_FRACTION * n
         cost = [sum(k + n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
         if n >= 100 * w:
             assert max(cost) - min(cost) <= 2 * (k + n)  # within a row or two

@@ -100,7 +100,8 @@ def build_cli(force=False):
     if not os.path.exists(srcs[0]):
         return None
     out = os.path.join(ROOT, "parfastaai_amd/lib/par_fastaai_amd")
-    if force or _newer(out, srcs + hdrs + [os.path.join(ROOT, "include/pfaai_hip.h")]):
+    if force or _newer(out, srcs + hdrs + [os.path.join(ROOT, "include/pfaai_hip.h"),
+                                           os.path.join(ROOT, "include/pfaai_hip.hpp")]):
         _run(["g++", "-std=c++17", "-O2", "-Wall", "-fopenmp", "-I" + os.path.join(ROOT, "include"), "-o", out,
               *srcs, "-L" + os.path.join(ROOT, "parfastaai_amd/lib"), "-lpfaai_hip",
               "-Wl,-rpath,$ORIGIN", "/lib/x86_64-linux-gnu/libsqlite3.so.0", "-ldl"])
