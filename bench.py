@@ -507,8 +507,8 @@ def main():
         # the bytes the implemented passes move per F entry (G_CHECKED): hist 1
         # reads F 8 + writes the u16 column 2; scatter 1 reads 8, writes 8;
         # hist 2 reads 8; scatter 2 reads 8, writes G_pos 4; k_gend reads
-        # G_tet 4 + G_pos 4 + a 4-B run end, writes G_end 4 = 62 B
-        pass_per_f = {"g_checked": 62}.get(load_path)
+        # G_tet 4 + a 4-B run end, writes G_end 4; k_hash_f reads F 8 = 66 B
+        pass_per_f = {"g_checked": 66}.get(load_path)
         load = {"path": load_path, "device_ms": round(ms_load_dev, 3), "host_checks_ms": round(ms_checks, 1),
                 "h2d_ms": round(ms_upload, 1), "wall_ms": round(load_wall_ms, 1), "F": n_f,
                 "alg_bytes_per_F": alg_per_f,

@@ -131,10 +131,9 @@ constexpr int32_t kGposMaxIds = 20480;  // G_pos built for all-vs-all problems u
 enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3, RK_V2 = 4 };
 
 // scalars buffer layout (u64 each)
-// SC_HG / SC_HF / SC_HL / SC_HT: the both-given load's check sums -- h(pos, key)
-// over the sort's output, h(i, t) over F, h(pos, list) over G's lists, h(G_pos,
-// G_tet) over G (pfaai_sort.hpp DstGposHash, k_hash_f; k_gend)
-enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_HG = 5, SC_HF = 6, SC_HL = 7, SC_HT = 8, SC_N = 9 };
+// SC_HF / SC_HG: the both-given load's membership sums over F (k_hash_f) and
+// over G (k_gend), pfaai_sort.hpp DstGpos
+enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_HF = 5, SC_HG = 6, SC_N = 7 };
 
 inline int fail(pfaai_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;

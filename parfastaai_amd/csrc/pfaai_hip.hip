@@ -617,30 +617,30 @@ int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool wa
 
 // Both F and G given with |G| = |F|: G must be F's genome-major transpose.
 // One two-pass sort of F by (genome, protein) -- records (key, F index),
-// read straight from F -- yields G_pos (into gpos) and the sort side of the
-// list-bound sum (DstGposHash); k_hash_f the F side of the tetramer sum.  The
-// G sides come from k_gend (HASH), launched by load_impl, which then compares
-// all four (finish_g_check).
+// read straight from F -- yields G_pos (into gpos); k_hash_f sums the F side
+// of the membership check (pfaai_sort.hpp, DstGpos) on the second stream
+// beside the sort.  The G side comes from k_gend (HASH), launched by
+// load_impl, which then compares the two (finish_g_check).
 int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, hipStream_t s) {
     const int kb = bits_for((int64_t)c->prob.n_ids * c->prob.n_prot);
     int rc;
     if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    HIPCHK(c, hipMemsetAsync(sc + SC_HG, 0, 4 * sizeof(unsigned long long), s));  // SC_HG, SC_HF, SC_HL, SC_HT
+    HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 2 * sizeof(unsigned long long), s));  // SC_HF, SC_HG
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
-    const DstGposHash dst{gpos, seed, sc + SC_HG};
-    // the F side of the tetramer sum needs only Lp: it runs on the second
-    // stream beside the sort (VALU work beside HBM-bound passes); the load's
-    // stream waits for it after the sort
+    const DstGpos dst{gpos};
+    // the F side runs on the second stream beside the sort (its VALU work
+    // beside HBM-bound passes); the load's stream waits for it after the sort
     if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     hipEvent_t* ev = c->side_ev;
     for (int k = 0; k < 2; ++k)
         if (!ev[k]) HIPCHK(c, hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
     HIPCHK(c, hipEventRecord(ev[0], s));  // (after the sums were cleared)
     HIPCHK(c, hipStreamWaitEvent(c->copy_stream, ev[0], 0));
-    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->Lp.p), seed,
-                       sc + SC_HF);
+    hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->Lp.p),
+                       static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
+                       (uint32_t)c->prob.n_prot, seed, sc + SC_HF);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->copy_stream));
     if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
@@ -648,12 +648,12 @@ int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, 
     return PFAAI_RC_OK;
 }
 
-// After k_gend<*, true>: -1 unless both sum pairs agree.
+// After k_gend<*, true>: -1 unless the F and G membership sums agree.
 int finish_g_check(pfaai_ctx* c, hipStream_t s) {
-    unsigned long long h[4] = {0, 0, 0, 0};
-    HIPCHK(c, hipMemcpyAsync(h, static_cast<unsigned long long*>(c->scalars.p) + SC_HG, sizeof(h), hipMemcpyDeviceToHost, s));
+    unsigned long long h[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(h, static_cast<unsigned long long*>(c->scalars.p) + SC_HF, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    return (h[0] != h[2] || h[1] != h[3]) ? -1 : PFAAI_RC_OK;  // [HG, HF, HL, HT]
+    return h[0] != h[1] ? -1 : PFAAI_RC_OK;  // [HF, HG]
 }
 
 // G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
@@ -951,8 +951,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     // starts (hipMalloc inside it left the stream idle: 8.5-9.0 ms measured
     // for 7.8 ms of kernels at 10k)
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
-        if ((rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
-        if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;
+        if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
         if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     }
@@ -973,20 +972,28 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         }
     }
     bool has_g = in_g;
-    uint32_t* gpos_chk = nullptr;  // both given: the sort's G_pos, whose sums k_gend completes
+    bool g_check = false;  // both given: the membership sums, completed by k_gend's G side
     uint64_t check_seed = 0;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
-        // the transpose of F -- one sort of F by (genome, protein) proves it
-        // against the caller's lists (and yields G_pos): no search per entry
-        // (G_pos is the sort's output even when the row kernels will not use
-        // it: a scratch buffer then, released with the sort space)
-        if (!want_pos && (rc = ensure(c, c->rec_c, n_f * 4))) return rc;
-        gpos_chk = static_cast<uint32_t*>(want_pos ? c->G_pos.p : c->rec_c.p);
+        // the transpose of F, proven by the membership sums over F (k_hash_f)
+        // and over G (k_gend); G_pos, where the row kernels use it, from one
+        // sort of F by (genome, protein).  Without G_pos no sort runs.
         check_seed = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
                      (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
-        if ((rc = check_g_transpose(c, n_f, gpos_chk, check_seed, s))) return rc;
-        pos_ok = fp16_done = true;
+        g_check = true;
+        if (want_pos) {
+            if ((rc = check_g_transpose(c, n_f, static_cast<uint32_t*>(c->G_pos.p), check_seed, s))) return rc;
+            fp16_done = true;
+        } else {
+            auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+            HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 2 * sizeof(unsigned long long), s));
+            hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
+                               static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), (uint32_t)P,
+                               check_seed, sc + SC_HF);
+            HIPCHK(c, hipGetLastError());
+        }
+        pos_ok = true;
         c->load_path = PFAAI_LOAD_G_CHECKED;
     } else if (in_g && in_f && n_f) {  // both given, G larger (QT: both DBs' lists): G must hold F (k_g_check)
         auto* sc = static_cast<unsigned long long*>(c->scalars.p);
@@ -1081,29 +1088,29 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     {
         // k_gend: G_end (with G_pos) and / or the G sides of the both-given check
         const int ggrid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, kGendLists), 1), 1 << 16);
-        auto* sums = static_cast<unsigned long long*>(c->scalars.p) + SC_HL;
+        auto* sums = static_cast<unsigned long long*>(c->scalars.p) + SC_HG;
         if (d.G_pos) {
             if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
             if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
             const auto* ends = reinterpret_cast<const uint32_t*>(c->blk.p);
             auto* gend = static_cast<uint32_t*>(c->G_end.p);
-            if (gpos_chk)
+            if (g_check)
                 hipLaunchKernelGGL((k_gend<true, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, gpos_chk, check_seed, sums);
+                                   gend, check_seed, sums);
             else
                 hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, nullptr, 0ull, nullptr);
+                                   gend, 0ull, nullptr);
             HIPCHK(c, hipGetLastError());
             d.G_end = static_cast<const uint32_t*>(c->G_end.p);
         } else {
             release(c->G_end);
-            if (gpos_chk) {
+            if (g_check) {
                 hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
-                                   nullptr, nullptr, gpos_chk, check_seed, sums);
+                                   nullptr, nullptr, check_seed, sums);
                 HIPCHK(c, hipGetLastError());
             }
         }
-        if (gpos_chk && (rc = finish_g_check(c, s))) {
+        if (g_check && (rc = finish_g_check(c, s))) {
             if (rc == -1)
                 return fail(c, PFAAI_RC_INVALID,
                             "G does not hold exactly the memberships of F (it must be F's genome-major transpose)");

@@ -103,56 +103,61 @@ struct DstRecs {
 
 // Both F and G given (records key g * P + p | F index << 32, sorted = F's
 // genome-major transpose): G_pos[pos] = F index i, and the caller's G must BE
-// that transpose.  Both halves of that are proven by keyed hash sums, so the
-// write phase loads nothing (the first form read G_off[key], G_off[key + 1]
-// and G_tet[pos] for every record: ~3 random L2 requests per record, 3.4 ms
-// of a 10k load's pass):
-//   list bounds: the sum over sorted positions of hp(pos, key) (here) must
-//     equal the sum over G's lists of hp(pos, list) for every position of
-//     every list (k_gend) -- the key sequence the sort produced is then the
-//     one G_off describes;
-//   tetramers: the sum over G of h(G_pos[k], G_tet[k]) (k_gend) must equal
-//     the sum over F of h(i, t(i)) (k_hash_f, from Lp alone).  G_pos is a
-//     bijection onto F by construction, so the sums differ unless every
-//     tetramer matches.
-// Either sum pair agrees for different inputs with probability ~2^-64 (h
-// and hp are a 64-bit mix of an injective code, keyed by a per-load random
-// seed).
+// that transpose.  That is a statement about sets: F's memberships (g, p, t)
+// and G's must be the same (both hold distinct triples: F strictly sorted by
+// (t, p, g), every G list strictly ascending -- host-checked -- and |G| =
+// |F|).  Then list (g, p) holds exactly F's entries with key g * P + p, in
+// t order = F index order, so the sorted positions ARE G's positions.  The
+// set equality is proven by keyed hash sums: the sum over F of h(g * P + p,
+// t) (k_hash_f, streaming F block by block) must equal the sum over G of
+// h(list, G_tet) (k_gend) -- they agree for different sets with probability
+// ~2^-64 (h is a 64-bit mix of the injective 50-bit code key << 18 | t,
+// keyed by a per-load random seed).  So the sort's passes load nothing
+// beyond their records (the first form checked list bounds by G_off[key],
+// G_off[key + 1] and read G_tet[pos] per record in the last pass: ~3 random
+// L2 requests per record, 3.4 ms of a 10k load's pass).
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser (a bijection)
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     return x ^ (x >> 31);
 }
-__device__ __forceinline__ uint64_t pair_hash(uint64_t seed, uint64_t i, uint32_t t) {
-    return mix64(seed ^ ((i << 18) | t));  // i < 2^32, t < 2^18 (host-checked): an injective 50-bit code
-}
-__device__ __forceinline__ uint64_t pos_hash(uint64_t seed, uint32_t pos, uint32_t key) {
-    return mix64(~seed ^ (((uint64_t)pos << 32) | key));
+__device__ __forceinline__ uint64_t member_hash(uint64_t seed, uint32_t key, uint32_t t) {
+    return mix64(seed ^ (((uint64_t)key << 18) | t));  // key < 2^32, t < 2^18 (host-checked): injective
 }
 
-struct DstGposHash {
+struct DstGpos {
     uint32_t* G_pos;
-    uint64_t seed;
-    unsigned long long* sum;
     static constexpr int kWH = kSortItems;
-    static constexpr bool kSum = true;
+    static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
     __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
         G_pos[pos] = (uint32_t)(v >> 32);
-        return pos_hash(seed, (uint32_t)pos, (uint32_t)v);
+        return 0;
     }
 };
 
-// the F side of DstGposHash's sum: h(i, t) over every F entry i of every
-// tetramer block t -- from Lp alone, no F read
-__global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, uint64_t seed,
+// the F side of the membership sum: h(g * P + p, t) over every F entry of
+// every tetramer block t (one workgroup per block, grid-stride; four entries
+// per thread in flight, indices clamped rather than loads under a branch)
+__global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
+                                                const int32_t* __restrict__ Fg, uint32_t P, uint64_t seed,
                                                 unsigned long long* __restrict__ sum) {
     uint64_t acc = 0;
     for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
-        const int64_t e = Lp[t + 1];
-        for (int64_t i = Lp[t] + threadIdx.x; i < e; i += blockDim.x) acc += pair_hash(seed, (uint64_t)i, (uint32_t)t);
+        const int64_t b = Lp[t], e = Lp[t + 1];
+        for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * 256) {
+            uint32_t key[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = min(i0 + u * 256, e - 1);
+                key[u] = (uint32_t)__builtin_nontemporal_load(Fg + i) * P + (uint32_t)__builtin_nontemporal_load(Fp + i);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * 256 < e) acc += member_hash(seed, key[u], (uint32_t)t);
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -654,8 +659,8 @@ __global__ void k_len_from_t(const int32_t* __restrict__ T, int32_t P, int32_t n
 //   END:  G_end[k] = the end of the F run (t, p) of G entry k of list (g, p),
 //         from the run-end table (k_blk_end, u32, p-major) -- looked up once
 //         per load, so the WK 3 row kernel reads (G_pos, G_end) coalesced;
-//   HASH: the G sides of the both-given check (DstGposHash): sums[0] +=
-//         hp(k, list of k), sums[1] += h(G_pos[k], G_tet[k]).
+//   HASH: the G side of the both-given check (DstGpos): sums[0] +=
+//         h(list of k, G_tet[k]).
 // The lists are taken protein-major (all genomes of protein p, then p + 1),
 // so the table lookups in flight hit one or two protein rows (640 KB each),
 // which stay in every XCD's L2 -- genome-major order touched all 100 rows at
@@ -668,15 +673,15 @@ constexpr int kGendLists = 32;
 template <bool END, bool HASH>
 __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
                                               int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
-                                              uint32_t* __restrict__ G_end, const uint32_t* __restrict__ G_pos,
-                                              uint64_t seed, unsigned long long* __restrict__ sums) {
+                                              uint32_t* __restrict__ G_end, uint64_t seed,
+                                              unsigned long long* __restrict__ sums) {
     __shared__ int64_t lb[kGendLists];
     __shared__ uint32_t pre[kGendLists + 1];
     __shared__ int64_t row[kGendLists];
     __shared__ uint32_t lid[kGendLists];
     const int tid = threadIdx.x;
     const int64_t n_ids = n_lists / P;
-    uint64_t hl = 0, ht = 0;
+    uint64_t hm = 0;
     for (int64_t q0 = (int64_t)blockIdx.x * kGendLists; q0 < n_lists; q0 += (int64_t)gridDim.x * kGendLists) {
         if (tid < 64) {  // one wave: the block's lists, their lengths and an inclusive scan
             uint32_t len = 0;
@@ -716,12 +721,9 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
                 li[u] = lid[lo];
             }
             int32_t t[4];
-            uint32_t gp[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {  // (streamed once: non-temporal, the L2 keeps the table rows)
+            for (int u = 0; u < 4; ++u)  // (streamed once: non-temporal, the L2 keeps the table rows)
                 t[u] = __builtin_nontemporal_load(G_tet + k[u]);
-                if constexpr (HASH) gp[u] = __builtin_nontemporal_load(G_pos + k[u]);
-            }
             uint32_t v[4];
             if constexpr (END) {
 #pragma unroll
@@ -731,10 +733,7 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
             for (int u = 0; u < 4; ++u) {
                 if (f0 + (uint32_t)u * 256u < total) {
                     if constexpr (END) G_end[k[u]] = v[u];
-                    if constexpr (HASH) {
-                        hl += pos_hash(seed, (uint32_t)k[u], li[u]);
-                        ht += pair_hash(seed, gp[u], (uint32_t)t[u]);
-                    }
+                    if constexpr (HASH) hm += member_hash(seed, li[u], (uint32_t)t[u]);
                 }
             }
         }
@@ -742,14 +741,8 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
     }
     if constexpr (HASH) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            hl += __shfl_down(hl, o, 64);
-            ht += __shfl_down(ht, o, 64);
-        }
-        if ((tid & 63) == 0) {
-            atomicAdd(&sums[0], (unsigned long long)hl);
-            atomicAdd(&sums[1], (unsigned long long)ht);
-        }
+        for (int o = 32; o > 0; o >>= 1) hm += __shfl_down(hm, o, 64);
+        if ((tid & 63) == 0 && hm) atomicAdd(&sums[0], (unsigned long long)hm);
     }
 }
 
