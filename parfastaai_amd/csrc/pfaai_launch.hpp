@@ -229,6 +229,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             if (sv == "noskip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "n16") { launch_pl<MODE, 5, 1024, 8, 1, true, 1024>(c, rb, re, flags, aji, S, N, s); return; }
             if (sv == "s1skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 128>(c, rb, re, flags, aji, S, N, s); return; }
+            if (sv == "bf") { launch_pl<MODE, 5, 1024, 8, 1, true, 256>(c, rb, re, flags, aji, S, N, s); return; }
         }
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)

@@ -150,6 +150,22 @@ __device__ __forceinline__ void pl_add_m(const Dev& d, int32_t a, int32_t b, boo
     }
 }
 
+// Branch-free WK 3 member adds (VAR bit 256, A/B): an invalid slot adds 0
+// to a lane-private word of the counter row (acc[lane], no bank conflict, no
+// change) instead of an exec-masked branch per slot (3 SALU + a branch).
+__device__ __forceinline__ void pl_add_bf(uint32_t b, bool valid, uint32_t* accb, uint32_t lane_wi) {
+    uint32_t wi;
+    asm("v_lshrrev_b32 %0, 1, %1" : "=v"(wi) : "v"(b));
+    const uint32_t inc = valid ? 1u << ((b & 1u) << 4) : 0u;
+    __hip_atomic_fetch_add(&accb[valid ? wi : lane_wi], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void pl_scatter4_bf(uint4 b, uint32_t m, uint32_t* accb, uint32_t lane_wi) {
+    pl_add_bf(b.x, m & 1u, accb, lane_wi);
+    pl_add_bf(b.y, m & 2u, accb, lane_wi);
+    pl_add_bf(b.z, m & 4u, accb, lane_wi);
+    pl_add_bf(b.w, m & 8u, accb, lane_wi);
+}
+
 template <int MODE, int WK>
 __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, uint32_t m, uint32_t* accb,
                                               int32_t wlo, uint32_t wspan) {
@@ -544,8 +560,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         return pl_issue_m2<TC, BIGF, GP>(r_fg, d.Fg, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
     };
     auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
-        pl_scatter4_m<MODE, WK>(d, a, bb, m & 15u, acc_x - (cc0 >> 1), wlo, wspan);
-        pl_scatter4_m<MODE, WK>(d, a, bbh, m >> 4, acc_x - (cc0 >> 1), wlo, wspan);
+        if constexpr (WK == 3 && MODE == 0 && (VAR & 256) != 0) {
+            const uint32_t lane_wi = (uint32_t)(cc0 >> 1) + (uint32_t)lane;  // accb[lane_wi] = acc_x[lane]
+            pl_scatter4_bf(bb, m & 15u, acc_x - (cc0 >> 1), lane_wi);
+            pl_scatter4_bf(bbh, m >> 4, acc_x - (cc0 >> 1), lane_wi);
+        } else {
+            pl_scatter4_m<MODE, WK>(d, a, bb, m & 15u, acc_x - (cc0 >> 1), wlo, wspan);
+            pl_scatter4_m<MODE, WK>(d, a, bbh, m >> 4, acc_x - (cc0 >> 1), wlo, wspan);
+        }
     };
 
     if constexpr (LA) {
