@@ -22,9 +22,11 @@
 //                  ballots give each lane its peers with the same digit) and
 //                  per-wave u16 digit counters in LDS, the tile reordered by
 //                  digit in LDS, then written out in that order: each digit's
-//                  run of the tile is contiguous in the output (8 records of 8
+//                  run of the tile is contiguous in the output (4 records of 8
 //                  B on average at DB = 10), so consecutive lanes store to
-//                  consecutive addresses.
+//                  consecutive addresses; the tiles in flight on an XCD are
+//                  consecutive (per-XCD tile counters), so neighbouring runs
+//                  complete whole lines in its L2.
 // The sources of the first pass and the destination of the last are functors,
 // so the first pass reads the caller's arrays directly (no key array) and the
 // last writes the product columns -- and, when both orientations were given,
@@ -37,10 +39,12 @@ namespace pfaai {
 constexpr int kSortThreads = 1024;                      // k_sort_grp / k_sort_top
 constexpr int kSortItems = 8;                           // records per thread and tile
 // threads of the hist / scatter workgroups: 512 (tiles of 4096 records; the
-// scatter's LDS, 56 KB at 10-bit digits, lets two workgroups share a CU, so
-// one's barriers and write-phase loads overlap the other's ranking) -- one
-// 1024-thread workgroup per CU (8192-record tiles, ~104 KB of LDS) left the
-// CU idle at every barrier: 2.9-3.3 ms per pass at 10k, ~1.5 TB/s
+// scatter's LDS, 56 KB at 10-bit digits, lets two workgroups share a CU).
+// With the per-XCD tile counters and non-temporal loads it measures 1.84 /
+// 1.63 ms for the 10k F -> G passes against 2.13 / 1.85 for one 1024-thread
+// workgroup per CU (8192-record tiles, ~104 KB of LDS), and the next-tile
+// prefetch (PF) costs more registers than it hides: 2.07 / 1.61
+// (profiles/r03u_sort/)
 constexpr int kSortNT = 512;
 constexpr bool kSortPF = false;                          // next-tile prefetch (k_sort_scatter PF)
 constexpr int kSortTileMin = 512 * kSortItems;          // the smallest tile (sizes the hist buffer)
