@@ -87,6 +87,46 @@ def test_both_given_refuses_a_g_that_is_not_the_transpose(engine):
     assert engine.load_info() == "g_checked"
 
 
+def test_both_given_without_gpos_checks_membership_without_a_sort(engine):
+    """Where the row kernels use no G_pos (-q subsets; all-vs-all past 20 480
+    genomes) the both-given load runs only the membership sums (k_hash_f over
+    F, k_gend over G) and no sort: a G with one tetramer replaced is still
+    refused, and the real transpose gives the oracle's S / N."""
+    from parfastaai_amd.datastruct import ParFAAIQSubData
+
+    g = syn.generate(400, 20, clade_size=10)
+    q = [g["genome_set"][i] for i in range(2, 400, 9)]
+    pb = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"], q
+                                    ).with_genome_major(g["G_off"], g["G_tet"]).problem()
+    G_off, G_tet = pb["G_off"], pb["G_tet"]
+    bad = G_tet.copy()
+    k0, k1 = int(G_off[7 * 20 + 2]), int(G_off[7 * 20 + 3])
+    lst = set(bad[k0:k1].tolist())
+    new = next(t for t in range(159999, 0, -1) if t not in lst)
+    bad[k0:k1] = np.sort(np.r_[bad[k0:k1 - 1], new])
+    with pytest.raises(_capi.PfaaiError):
+        engine.load(**dict(pb, G_tet=bad))
+    # a membership moved to another genome's list of the same protein: same
+    # |G|, every list still ascending, the triple (g, p, t) changed
+    g_a, g_b, p = 3, 4, 5
+    la = G_tet[G_off[g_a * 20 + p]:G_off[g_a * 20 + p + 1]]
+    lb = G_tet[G_off[g_b * 20 + p]:G_off[g_b * 20 + p + 1]]
+    t = next((x for x in la.tolist() if x not in set(lb.tolist())), None)
+    if t is not None and len(la) > 1:
+        lists = [G_tet[G_off[k]:G_off[k + 1]].tolist() for k in range(len(G_off) - 1)]
+        lists[g_a * 20 + p].remove(t)
+        lists[g_b * 20 + p] = sorted(lists[g_b * 20 + p] + [t])
+        off2 = np.r_[0, np.cumsum([len(x) for x in lists])].astype(G_off.dtype)
+        tet2 = np.concatenate([np.asarray(x, dtype=G_tet.dtype) for x in lists])
+        with pytest.raises(_capi.PfaaiError):
+            engine.load(**dict(pb, G_off=off2, G_tet=tet2))
+    engine.load(**pb)
+    assert engine.load_info() == "g_checked"
+    aji, S, N = engine.compute(0)
+    want = O.Problem(pb).ref_run()
+    assert np.array_equal(S, want["S"]) and np.array_equal(N, want["N"])
+
+
 def test_f_only_inconsistent_t_takes_the_general_sort(engine):
     """T is an input of the formula (J = c / (T[p][A] + T[p][B] - c)); when it
     is not the list lengths of F, G_off cannot come from it: the general
