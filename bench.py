@@ -50,7 +50,8 @@ import numpy as np  # noqa: E402
 E2E_PROFILE = "r03d_e2e_cli_c2.json"  # tools/gpu/e2e_c2.py's latest committed run
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
-ROWS_KERNEL = "pfaai::k_rows_pl (fused scatter + Jaccard + AJI, default row kernel)"
+ROWS_KERNEL = ("pfaai::k_rows_pl (fused scatter + Jaccard + AJI; the wide rows as 1024-thread workgroups, the "
+               "rows of <= 2047 columns as 512-thread ones on a second stream, one pfaai_run)")
 
 
 def log(msg):

@@ -207,7 +207,7 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
 // (k_blk_end) instead of k_blk's 16-B entries.  One predicate for the run
 // table build (run_mode) and the kernel choice (launch_pl).
 inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
-    return mode == 0 && c->rows_kernel == RK_PL && c->dev.G_pos && !c->windows &&
+    return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pos && !c->windows &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
            !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");
 }

@@ -164,6 +164,57 @@ void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double*
                            rowptr, recs, chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
 }
 
+// The narrow all-vs-all rows (<= kNarrowCols columns) as 512-thread WK 3
+// workgroups, four per CU: a narrow row's time is its 100-protein chain, not
+// its width, so twice the rows in flight per CU finish the narrow end sooner
+// (the narrowest 8-way shard of 10k 1.11 -> 0.96 ms).  A launch reaching into
+// the narrow end runs those rows on the second stream, concurrently with its
+// wide rows on the caller's (10k all-vs-all 7.72 -> 7.58 ms;
+// profiles/r03v/); a launch of narrow rows only runs them on the caller's
+// stream.  Returns false where it does not apply (not the WK 3 path, or no
+// narrow row in [rb, re)).  PFAAI_PL_NO512=1 (diagnostics) turns it off.
+// (a row of c columns needs (c + 1) / 2 counter words -- its chunk starts at
+// an even column -- so two words per thread of 512 cover 2 047 columns)
+constexpr int kNarrowCols = 2 * 2 * 512 - 1;
+
+inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+                          hipStream_t s) {
+    if (DIAG_ENV("PFAAI_PL_NO512") || !pl_uses_ends(c, 0) || !c->copy_stream || !c->side_ev[0] || !c->side_ev[1])
+        return false;
+    const int64_t n = c->prob.n_ids;  // all-vs-all: row r is genome r, n - 1 - r columns
+    const int64_t cut = std::max(rb, std::min(re, n - 1 - (int64_t)kNarrowCols));
+    if (cut >= re) return false;
+    const int32_t cols_all = c->cols_run;
+    if (ceil_div((int64_t)(n - 1 - cut) + 1, 2 * 2 * 512) != 1) return false;  // one chunk, or not the WK 3 form
+    auto narrow = [&](hipStream_t st) {
+        c->cols_run = (int32_t)(n - 1 - cut);  // the narrow launch's widest row
+        if (pick_kw<512>(c->cols_run, 2) == 1)
+            launch_pl<0, 1, 512, 8, 1, true>(c, cut, re, flags, aji, S, N, st);
+        else
+            launch_pl<0, 2, 512, 8, 1, true>(c, cut, re, flags, aji, S, N, st);
+        c->cols_run = cols_all;
+    };
+    if (cut == rb) {
+        narrow(s);
+        return true;
+    }
+    // fork: the narrow rows on the second stream after everything before this
+    // launch on s; join: s waits for them before what follows (the run's end event)
+    if (hipEventRecord(c->side_ev[0], s) != hipSuccess || hipStreamWaitEvent(c->copy_stream, c->side_ev[0], 0) != hipSuccess)
+        return false;
+    narrow(c->copy_stream);
+    switch (pick_kw<1024>(cols_all, 5)) {
+        case 1: launch_pl<0, 1, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+        case 2: launch_pl<0, 2, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+        case 3: launch_pl<0, 3, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+        case 4: launch_pl<0, 4, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+        default: launch_pl<0, 5, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+    }
+    (void)hipEventRecord(c->side_ev[1], c->copy_stream);
+    (void)hipStreamWaitEvent(s, c->side_ev[1], 0);
+    return true;
+}
+
 template <int MODE>
 void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                  hipStream_t s) {
@@ -185,6 +236,20 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         }
 #endif
         if (c->rows_kernel == RK_PL512) {
+            // 512-thread workgroups, four per CU (<= 64 VGPRs) with N in LDS
+            // where P <= 255 -- and the WK 3 walks (pl_uses_ends) -- for A/B
+            // of narrow launches (more rows in flight per CU)
+            if (c->prob.n_prot <= 255) {
+                switch (pick_kw<512>(c->cols_run, 10)) {
+                    case 1: launch_pl<MODE, 1, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                    case 2: launch_pl<MODE, 2, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                    case 3: launch_pl<MODE, 3, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                    case 4: launch_pl<MODE, 4, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
+                    PL_CASE(512, 5) PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
+                    default: break;
+                }
+                return;
+            }
             switch (pick_kw<512>(c->cols_run, 10)) {
                 PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
                 PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
@@ -234,6 +299,9 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
 #endif
         // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
         const bool nl = c->prob.n_prot <= 255 && !DIAG_ENV("PFAAI_PL_NREG");
+        if constexpr (MODE == 0) {
+            if (nl && launch_narrow(c, rb, re, flags, aji, S, N, s)) return;
+        }
         if (nl) {
             switch (kw) {
                 case 1: launch_pl<MODE, 1, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
