@@ -81,18 +81,35 @@ def main():
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump({"source": "rocprofv3 --pmc --kernel-trace, tools/gpu/pmc.sh, 10k SYN all-vs-all",
                    "kernels": res}, f, indent=1, sort_keys=True)
-    rows = [k for k in res if "k_rows" in k]
+    # One all-vs-all step may run two row kernels at once (pfaai_launch.hpp
+    # launch_narrow: the wide rows as 1024-thread workgroups on the step's
+    # stream, the narrow end as 512-thread ones on the side stream).  The step
+    # figures add both: bytes and instructions summed; VALU busy over the sum
+    # of their cycles, since counter collection serialises the dispatches.
+    rows = sorted((k for k in res if "k_rows" in k),
+                  key=lambda k: -res[k]["derived"].get("kernel_cycles", 0))
     if rows:
         k = rows[0]
         dv = res[k]["derived"]
+
+        def total(get):
+            xs = [get(r) for r in rows]
+            return sum(xs) if all(x is not None for x in xs) else None
+
+        valu_q = total(lambda r: res[r]["counters"].get("SQ_ACTIVE_INST_VALU"))
+        cyc = total(lambda r: res[r]["derived"].get("kernel_cycles"))
         with open(os.path.join(prof, "pmc_k_rows.json"), "w") as f:
-            json.dump({"kernel": k, "hbm_bytes_per_launch": dv.get("hbm_bytes"),
-                       "hbm_read_bytes_x2_bound": dv.get("hbm_read_bytes_x2_bound"),
-                       "valu_busy": dv.get("valu_busy"), "wave_frac_waiting": dv.get("wave_frac_waiting"),
+            json.dump({"kernel": k, "kernels": rows,
+                       "hbm_bytes_per_launch": total(lambda r: res[r]["derived"].get("hbm_bytes")),
+                       "hbm_read_bytes_x2_bound": total(lambda r: res[r]["derived"].get("hbm_read_bytes_x2_bound")),
+                       "valu_busy": valu_q * 4 / 1024 / cyc if valu_q and cyc else dv.get("valu_busy"),
+                       "valu_busy_main": dv.get("valu_busy"),
+                       "wave_frac_waiting": dv.get("wave_frac_waiting"),
                        "lds_conflict_frac": dv.get("lds_conflict_frac"),
-                       "valu_insts": res[k]["counters"].get("SQ_INSTS_VALU"),
-                       "salu_insts": res[k]["counters"].get("SQ_INSTS_SALU"),
-                       "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024, one launch covers all 10k rows",
+                       "valu_insts": total(lambda r: res[r]["counters"].get("SQ_INSTS_VALU")),
+                       "salu_insts": total(lambda r: res[r]["counters"].get("SQ_INSTS_SALU")),
+                       "note": "FETCH_SIZE+WRITE_SIZE KiB x 1024 summed over the step's row kernels "
+                               "(one step covers all 10k rows)",
                        "tag": tag}, f, indent=1)
     for k, v in res.items():
         dv = v["derived"]
