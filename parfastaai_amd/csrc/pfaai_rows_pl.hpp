@@ -744,17 +744,19 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     for (int k = 0; k < KW; ++k) {
         const int32_t w = tid + k * NT;
         if (w >= ncw) continue;
+        double sv[2];
+        int32_t nv[2];
+        bool ok[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int32_t b = cc0 + 2 * w + h;
-            if (b < wlo || b >= whi || !col_valid<MODE>(d, a, b)) continue;
-            const int64_t idx = pair_index<MODE>(d, a, b, compat);
+            ok[h] = b >= wlo && b < whi && col_valid<MODE>(d, a, b);
             double s = S[2 * k + h];
             int32_t n = NPK ? (int32_t)((n32[tid + (k >> 1) * NT] >> (8 * (k & 1) + 16 * h)) & 0xFFu)
                         : NK == 1 ? (int32_t)((n16[w] >> (8 * h)) & 0xFFu)
                         : NK == 2 ? (int32_t)((N[(k >> 1) % NN] >> (8 * (k & 1) + 16 * h)) & 0xFFu)
                                   : (int32_t)((N[k % NN] >> (16 * h)) & 0xFFFFu);
-            if (n == 0 && compat) {
+            if (ok[h] && n == 0 && compat) {
                 // extents stay 0/0 -> J of E[0]'s protein, N = 1
                 const unsigned long long key = *first_key;
                 const int32_t p0 = key == ~0ull ? 0 : (int32_t)(key & ((1ull << 21) - 1));
@@ -762,10 +764,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 s = 0.0 + 1.0 / (double)(Tp[tca] + Tp[d.tcol_col[b]] - 1);
                 n = 1;
             }
-            if (aji) aji[idx] = n ? s / (double)n : 0.0;
-            if (s_out) s_out[idx] = s;
-            if (n_out) n_out[idx] = n;
+            sv[h] = s;
+            nv[h] = n;
         }
+        put_pair<MODE>(d, a, cc0 + 2 * w, ok, sv, nv, compat, aji, s_out, n_out);
     }
 }
 
