@@ -38,7 +38,7 @@
 // wrong.
 //
 // NT threads per workgroup and WPE waves per SIMD: the default is NT = 1024
-// with WPE = 8, i.e. <= 64 VGPRs (a few spilled at KW = 5) so that two
+// with WPE = 8, i.e. <= 64 VGPRs (no spills in the WK 3 forms) so that two
 // workgroups share a CU and one's barrier waits overlap the other's work
 // (12.2 ms at 10k vs 15.6 ms at one per CU); NT = 512 is the alternative
 // form (twice the counter words per thread).
