@@ -129,8 +129,9 @@ __device__ __forceinline__ int64_t pair_index(const Dev& d, int32_t a, int32_t b
 // writes both with one 16-B store and a wave's stores cover whole lines; two
 // 8-B stores per lane wrote every line twice, half-masked (0.79 GB of
 // WRITE_SIZE for 0.40 GB of AJI at 10k all-vs-all, 7.58 -> 7.45 ms per step,
-// profiles/r03y).  The paired types are element-aligned: a row's first
-// output index has either parity.
+// profiles/r03y); non-temporal AJI stores on top made no difference (7.441
+// vs 7.445 ms, profiles/r03z/ab_nt_aji_store.txt).  The paired types are
+// element-aligned: a row's first output index has either parity.
 typedef double f64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
 typedef int32_t i32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 
