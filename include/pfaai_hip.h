@@ -248,6 +248,19 @@ int pfaai_load_info(const pfaai_ctx* ctx, int32_t* path);
  * ran by absolute column windows (rows wider than one kernel chunk). */
 int pfaai_run_info(const pfaai_ctx* ctx, int32_t* rows_kernel, int32_t* column_windows);
 
+/* How the last pfaai_run's k_rows_pl launches walked the F runs of each row
+ * genome's G entries (the reference's E construction for that row,
+ * ds_helper.hpp:270-357, without E):
+ *   SPLITTERS  run-table lookups, members pruned to the column chunk by the
+ *              table's line splitters (query rows, column windows, F only)
+ *   GPOS       all-vs-all: from the row genome's own F position + 1 (G_pos)
+ *              to its run end (G_end), both built at load -- the
+ *              benchmarked form; no run table in the step
+ * and whether the narrow rows (<= 2 047 columns) ran as a 512-thread launch
+ * on the context's side stream beside the wide rows.  -1: no k_rows_pl ran. */
+enum { PFAAI_WALK_NONE = -1, PFAAI_WALK_SPLITTERS = 0, PFAAI_WALK_GPOS = 3 };
+int pfaai_run_walk(const pfaai_ctx* ctx, int32_t* walk, int32_t* narrow_launch);
+
 /* |E| of the last run, counted by the scatter kernel (equals the reference's
  * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and
  * device times (ms) of its two phases: work-list build, row kernel.

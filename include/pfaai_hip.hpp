@@ -242,6 +242,7 @@ class ParFAAIHipImpl {
         if (m_ctx.size() == 1) {
             pfaai_last_stats(ctx(), &m_events, &m_msBuild, &m_msRows);
             pfaai_run_info(ctx(), &m_rowsKernel, nullptr);
+            pfaai_run_walk(ctx(), &m_walk, &m_narrow);
         }
         return 0;  // PFAAI_OK
     }
@@ -311,6 +312,9 @@ class ParFAAIHipImpl {
     int mode() const { return m_mode; }
     // PFAAI_ROWS_* of the last run
     int rowsKernel() const { return m_rowsKernel; }
+    // PFAAI_WALK_* of the last run, and whether its narrow rows ran beside it
+    int walkForm() const { return m_walk; }
+    bool narrowLaunch() const { return m_narrow != 0; }
     int nDevices() const { return (int)m_ctx.size(); }
     pfaai_ctx* context() const { return ctx(); }
 
@@ -337,6 +341,7 @@ class ParFAAIHipImpl {
             float b = 0.f, r = 0.f;
             pfaai_last_stats(m_ctx[i].get(), &e, &b, &r);
             pfaai_run_info(m_ctx[i].get(), &m_rowsKernel, nullptr);
+            pfaai_run_walk(m_ctx[i].get(), &m_walk, &m_narrow);
             m_events += e;
             m_msBuild = std::max(m_msBuild, b);
             m_msRows = std::max(m_msRows, r);
@@ -428,6 +433,7 @@ class ParFAAIHipImpl {
     int64_t m_events = 0;
     float m_msBuild = 0.f, m_msRows = 0.f;
     int32_t m_rowsKernel = -1;
+    int32_t m_walk = PFAAI_WALK_NONE, m_narrow = 0;
 };
 
 }  // namespace pfaai

@@ -44,6 +44,8 @@ def lib():
         L.oracle_dense_rows.restype = i64
         L.oracle_dense_rows.argtypes = [vp, vp, vp, vp, vp, i32, i32, vp, vp]
         L.oracle_init_jac.restype, L.oracle_init_jac.argtypes = None, [vp, vp, vp]
+        L.oracle_full_rows.restype = i64
+        L.oracle_full_rows.argtypes = [vp, vp, vp, vp, vp, i64, i64, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -122,3 +124,16 @@ class Problem:
         ne = lib().oracle_dense_rows(ctypes.byref(self.mode), _p(self.Lp), _p(self.Fp), _p(self.Fg), _p(self.T),
                                      row_lo, row_hi, _p(S), _p(N))
         return S, N, ne
+
+    def full_rows(self, row_lo, row_hi, S, N, AJI):
+        """Appendix A over output rows [row_lo, row_hi) (mode 0: genomes;
+        mode 2: query rows), written into S / N / AJI (views of the JAC-order
+        arrays starting at the rows' first JAC index; corrected semantics).
+        OpenMP over rows.  -> |E| of the rows."""
+        for a, dt in ((S, np.float64), (N, np.int32), (AJI, np.float64)):
+            assert a.dtype == dt and a.flags.c_contiguous
+        ne = lib().oracle_full_rows(ctypes.byref(self.mode), _p(self.Lp), _p(self.Fp), _p(self.Fg), _p(self.T),
+                                    row_lo, row_hi, _p(S), _p(N), _p(AJI))
+        if ne < 0:
+            raise RuntimeError(f"oracle_full_rows failed: {ne}")
+        return ne

@@ -348,3 +348,114 @@ int64_t oracle_dense_rows(const oracle_mode* m, const int64_t* Lp,
     free(cnt);
     return events;
 }
+
+/*
+ * SURVEY.md Appendix A for whole output rows, written in JAC-index order --
+ * the form the full-output digests (tests/golden/make_full_digests.py) hash.
+ * Same counts and the same fp64 reduction as oracle_dense_rows: c(p, a, b) =
+ * the number of tetramer blocks whose protein-p run (ds_helper.hpp:312-331)
+ * holds both a and b, S = sum over ascending p of c / (T[p][a] + T[p][b] - c)
+ * (algorithm_impl.hpp:222-277: E sorted by (gA, gB, p), so the sub-blocks of
+ * a pair come in protein order), N = proteins with c > 0, AJI = S / N
+ * (algorithm_impl.hpp:318); a pair with no event gets 0 (corrected
+ * semantics; compat is not supported here).  Derived from F alone: one walk
+ * of F collects, for every row genome in the window, the runs (t, p) it is a
+ * member of (in t order per protein), then the rows are counted
+ * independently (OpenMP over rows, per-thread u16 counters).
+ *
+ * Rows [row_lo, row_hi) in the mode's row space: mode 0 row r = genome r,
+ * columns b > r, JAC index n*r + b - (r+2)(r+1)/2 (ds_impl.hpp:83-86); mode 2
+ * row q = query genome n_tgt + q, columns the targets b < n_tgt, JAC index
+ * q*n_tgt + b (ds_impl.hpp:411-417).  Mode 1 is not supported (-3).  Outputs
+ * are indexed by JAC index - (the first JAC index of row_lo).  Returns |E| of
+ * the rows, or a negative error.
+ */
+int64_t oracle_full_rows(const oracle_mode* m, const int64_t* Lp, const int32_t* Fp, const int32_t* Fg,
+                         const int32_t* T, int64_t row_lo, int64_t row_hi, double* S, int32_t* N, double* AJI) {
+    if (m->mode == 1) return -3;
+    const int64_t ni = m->n_ids, P = m->n_prot, tc = m->t_cols;
+    const int64_t nrows = m->mode == 0 ? ni : m->n_qry;
+    if (row_lo < 0 || row_hi > nrows || row_lo > row_hi) return -4;
+    const int64_t nr = row_hi - row_lo;
+    if (nr == 0) return 0;
+    const int64_t g_lo = m->mode == 0 ? row_lo : m->n_tgt + row_lo; /* row genomes [g_lo, g_lo + nr) */
+    /* the runs of every row genome, grouped by (row, protein), t-ascending */
+    int64_t* off = (int64_t*)calloc((size_t)(nr * P + 1), sizeof(int64_t));
+    if (!off) return -1;
+    for (int t = 0; t < ORACLE_NTETRAMERS; t++)
+        for (int64_t i = Lp[t]; i < Lp[t + 1]; i++) {
+            const int64_t r = (int64_t)Fg[i] - g_lo;
+            if (r >= 0 && r < nr) off[r * P + Fp[i] + 1]++;
+        }
+    for (int64_t k = 0; k < nr * P; k++) off[k + 1] += off[k];
+    const int64_t nl = off[nr * P];
+    uint32_t* run = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)(nl > 0 ? nl : 1));
+    int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nr * P));
+    if (!run || !cur) { free(off); free(run); free(cur); return -1; }
+    memcpy(cur, off, sizeof(int64_t) * (size_t)(nr * P));
+    for (int t = 0; t < ORACLE_NTETRAMERS; t++) {
+        int64_t l = Lp[t];
+        while (l < Lp[t + 1]) {
+            int64_t r = l;
+            while (r < Lp[t + 1] && Fp[r] == Fp[l]) r++;
+            for (int64_t i = l; i < r; i++) {
+                const int64_t w = (int64_t)Fg[i] - g_lo;
+                if (w < 0 || w >= nr) continue;
+                const int64_t k = cur[w * P + Fp[l]]++;
+                run[2 * k] = (uint32_t)l;
+                run[2 * k + 1] = (uint32_t)r;
+            }
+            l = r;
+        }
+    }
+    free(cur);
+    const int64_t first = m->mode == 0 ? ni * row_lo - (row_lo + 1) * row_lo / 2 : row_lo * m->n_tgt;
+    int64_t events = 0;
+    int bad = 0;
+#pragma omp parallel reduction(+ : events)
+    {
+        uint16_t* cnt = (uint16_t*)calloc((size_t)ni, sizeof(uint16_t));
+        int32_t* touched = (int32_t*)malloc(sizeof(int32_t) * (size_t)ni);
+        double* srow = (double*)malloc(sizeof(double) * (size_t)ni);
+        int32_t* nrow = (int32_t*)malloc(sizeof(int32_t) * (size_t)ni);
+        if (!cnt || !touched || !srow || !nrow) {
+#pragma omp atomic write
+            bad = 1;
+        } else {
+#pragma omp for schedule(dynamic, 4)
+            for (int64_t w = 0; w < nr; w++) {
+                const int32_t a = (int32_t)(g_lo + w);
+                const int64_t c_lo = m->mode == 0 ? a + 1 : 0, c_hi = m->mode == 0 ? ni : m->n_tgt;
+                for (int64_t b = c_lo; b < c_hi; b++) { srow[b] = 0.0; nrow[b] = 0; }
+                for (int64_t p = 0; p < P; p++) { /* ascending protein order */
+                    int64_t nt = 0;
+                    for (int64_t k = off[w * P + p]; k < off[w * P + p + 1]; k++)
+                        for (uint32_t j = run[2 * k]; j < run[2 * k + 1]; j++) {
+                            const int32_t b = Fg[j];
+                            if (!is_valid(m, a, b)) continue;
+                            if (cnt[b]++ == 0) touched[nt++] = b;
+                        }
+                    for (int64_t x = 0; x < nt; x++) {
+                        const int32_t b = touched[x];
+                        const int64_t c = cnt[b];
+                        srow[b] += (double)c / (double)((int64_t)T[p * tc + a] + T[p * tc + b] - c);
+                        nrow[b] += 1;
+                        events += c;
+                        cnt[b] = 0;
+                    }
+                }
+                const int64_t base = (m->mode == 0 ? ni * a + c_lo - (int64_t)(a + 2) * (a + 1) / 2
+                                                   : (g_lo + w - m->n_tgt) * m->n_tgt) - first;
+                for (int64_t b = c_lo; b < c_hi; b++) {
+                    const int64_t k = base + (b - c_lo);
+                    S[k] = srow[b];
+                    N[k] = nrow[b];
+                    AJI[k] = nrow[b] ? srow[b] / nrow[b] : 0.0;
+                }
+            }
+        }
+        free(cnt); free(touched); free(srow); free(nrow);
+    }
+    free(run); free(off);
+    return bad ? -1 : events;
+}

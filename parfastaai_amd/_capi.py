@@ -37,11 +37,12 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_load_timing", "pfaai_stream_matrix",
+    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_timing", "pfaai_stream_matrix",
     "pfaai_load_info",
 ]
 LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
+WALKS = {-1: "none", 0: "splitters", 3: "gpos"}  # pfaai_run_walk
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
 #          const double* S, const int32_t* N)   (pfaai_sink_fn)
@@ -109,6 +110,7 @@ def load_library(path=None):
         "pfaai_stream_events": (ctypes.c_int, [vp, P64]),
         "pfaai_stream_matrix": (ctypes.c_int, [vp, i64, i64, i64, u32, MATRIX_SINK_FN, vp]),
         "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "pfaai_run_walk": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pfaai_load_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
         "pfaai_load_info": (ctypes.c_int, [vp, ctypes.POINTER(i32)]),
@@ -277,8 +279,11 @@ class Engine:
                     "pfaai_last_stats")
         rk, win = ctypes.c_int32(), ctypes.c_int32()
         self._check(self.lib.pfaai_run_info(self.ctx, ctypes.byref(rk), ctypes.byref(win)), "pfaai_run_info")
+        wk, nar = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.pfaai_run_walk(self.ctx, ctypes.byref(wk), ctypes.byref(nar)), "pfaai_run_walk")
         return {"n_events": ne.value, "ms_build": mb.value, "ms_rows": mr.value,
-                "rows_kernel": ROWS_KERNELS.get(rk.value, "?"), "column_windows": bool(win.value)}
+                "rows_kernel": ROWS_KERNELS.get(rk.value, "?"), "column_windows": bool(win.value),
+                "walk": WALKS.get(wk.value, "?"), "narrow_launch": bool(nar.value)}
 
     def load_timing(self):
         """(ms host checks, ms H2D, ms device F/G build) of the last load."""

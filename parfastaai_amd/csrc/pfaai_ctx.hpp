@@ -80,6 +80,11 @@ struct pfaai_ctx {
     DevBuf srec_a, srec_b, shist, sgsum, sbase;  // the load-time transposition sort (pfaai_sort.hpp)
     hipEvent_t load_ev[2] = {nullptr, nullptr};  // device span of the last load's F / G build
     hipEvent_t side_ev[2] = {nullptr, nullptr};  // the load's fork to / join from copy_stream (k_hash_f)
+    // the narrow all-vs-all rows' launch beside the wide rows (launch_narrow):
+    // its own stream and fork / join events, so the streamed outputs' D2H
+    // copies on copy_stream never queue it
+    hipStream_t side_stream = nullptr;
+    hipEvent_t narrow_ev[2] = {nullptr, nullptr};
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
     // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
@@ -92,6 +97,8 @@ struct pfaai_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     bool timed = false;
     int rows_kernel = 0;  // RowsKernel of the current run
+    int32_t last_walk = -1;      // PFAAI_WALK_* of the last run's k_rows_pl launches (pfaai_run_walk)
+    bool last_narrow = false;    // the last run's narrow rows ran beside it (launch_narrow)
     // per-run event triples for pfaai_timing (pool reused after each reset)
     std::vector<hipEvent_t> pool;
     size_t pool_used = 0;

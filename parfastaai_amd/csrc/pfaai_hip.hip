@@ -265,6 +265,8 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     HIPCHK(c, hipMemsetAsync(sc + SC_EVENTS, 0, sizeof(unsigned long long), s));
     const bool wl = c->rows_kernel == RK_WORKLIST;
+    c->last_walk = PFAAI_WALK_NONE;  // (set by launch_pl / launch_narrow)
+    c->last_narrow = false;
     // rows wider than one k_rows_pl chunk: absolute column windows, each with
     // its own run table (launch_pl); PFAAI_PL_WINDOWS=0 keeps the per-row
     // chunks over one table (A/B)
@@ -643,9 +645,30 @@ int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, 
                        (uint32_t)c->prob.n_prot, seed, sc + SC_HF);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->copy_stream));
-    if ((rc = tsort(c, src, dst, n_f, kb, s))) return rc;
-    HIPCHK(c, hipStreamWaitEvent(s, ev[1], 0));
+    rc = tsort(c, src, dst, n_f, kb, s);
+    // the join also on failure: a later load clears SC_HF on s, which must
+    // not overtake k_hash_f still adding into it on copy_stream
+    const hipError_t we = hipStreamWaitEvent(s, ev[1], 0);
+    if (rc) return rc;
+    HIPCHK(c, we);
     return PFAAI_RC_OK;
+}
+
+// G only, all-vs-all (the CLI's `<p>_genomes` load): G_pos, the F index of
+// every G entry, by the sort the both-given load runs (F by genome * P +
+// protein, records read straight from F, DstGpos) over the F that
+// build_f_from_g_sorted just built from G.  F is G's transpose by
+// construction, so the sorted positions are G's and nothing is checked; the
+// row kernels then take the benchmarked WK 3 form (G_pos + G_end) on this
+// path too.
+int build_gpos_from_f(pfaai_ctx* c, int64_t n_f, hipStream_t s) {
+    const int kb = bits_for((int64_t)c->prob.n_ids * c->prob.n_prot);
+    int rc;
+    if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
+    const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
+                       (uint32_t)c->prob.n_prot, nullptr};
+    const DstGpos dst{static_cast<uint32_t*>(c->G_pos.p)};
+    return tsort(c, src, dst, n_f, kb, s);
 }
 
 // After k_gend<*, true>: -1 unless the F and G membership sums agree.
@@ -660,7 +683,8 @@ int finish_g_check(pfaai_ctx* c, hipStream_t s) {
 // protein-major (k_gkeys_pm), one two-pass sort by tetramer (18-bit keys,
 // 9-bit digits) -> F (t, p, g) and Fp16 (DstFFromG), Lp from the sorted
 // tetramers (k_rowptr).  Needs P < 4096 and n_ids < 2^21 (the record
-// fields); else the caller takes build_f_from_g.  Builds no G_pos.
+// fields); else the caller takes build_f_from_g.  G_pos, where the row
+// kernels use it, comes from a second sort (build_gpos_from_f).
 int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t s) {
     const int32_t P = c->prob.n_prot, ni = c->prob.n_ids;
     int rc;
@@ -954,6 +978,11 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
         if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
+    } else if (in_g && !in_f && n_f && P < kMaxRuns && ng < ((int64_t)1 << 32)) {  // G only: both sorts' buffers
+        if ((rc = ensure_tsort(c, n_f, 18, true))) return rc;
+        if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
+        if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     }
     for (hipEvent_t& e : c->load_ev)
         if (!e) HIPCHK(c, hipEventCreate(&e));
@@ -965,6 +994,10 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
             if ((rc = build_f_from_g_sorted(c, ng, n_f, s))) return rc;
             fp16_done = true;
             c->load_path = PFAAI_LOAD_F_FROM_G;
+            if (want_pos && ng < ((int64_t)1 << 32)) {  // the WK 3 walks' G_pos (G_end follows below)
+                if ((rc = build_gpos_from_f(c, n_f, s))) return rc;
+                pos_ok = true;
+            }
         } else {
             if ((rc = build_f_from_g(c, ng, n_f, s))) return rc;
             c->load_path = PFAAI_LOAD_LEGACY;
@@ -1174,6 +1207,10 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) c->copy_stream = nullptr;
     for (hipEvent_t& e : c->side_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    // the narrow rows' stream (launch_narrow; without it they run on the caller's stream)
+    if (hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) c->side_stream = nullptr;
+    for (hipEvent_t& e : c->narrow_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
     for (hipEvent_t& e : c->load_ev)
         if (hipEventCreate(&e) != hipSuccess) e = nullptr;
     // every code object of the library loaded now rather than at the first
@@ -1207,6 +1244,8 @@ int pfaai_destroy(pfaai_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->side_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->narrow_ev)
+        if (e) (void)hipEventDestroy(e);
     release(c->st_dev);
     if (c->st_host) (void)hipHostFree(c->st_host);
     for (int i = 0; i < 2; ++i) {
@@ -1214,6 +1253,7 @@ int pfaai_destroy(pfaai_ctx* c) {
         if (c->st_copied[i]) (void)hipEventDestroy(c->st_copied[i]);
     }
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PFAAI_RC_OK;
@@ -1372,6 +1412,13 @@ int pfaai_run_info(const pfaai_ctx* c, int32_t* rows_kernel, int32_t* column_win
     if (!c) return PFAAI_RC_INVALID;
     if (rows_kernel) *rows_kernel = c->rows_kernel;
     if (column_windows) *column_windows = c->windows ? 1 : 0;
+    return PFAAI_RC_OK;
+}
+
+int pfaai_run_walk(const pfaai_ctx* c, int32_t* walk, int32_t* narrow_launch) {
+    if (!c) return PFAAI_RC_INVALID;
+    if (walk) *walk = c->last_walk;
+    if (narrow_launch) *narrow_launch = c->last_narrow ? 1 : 0;
     return PFAAI_RC_OK;
 }
 

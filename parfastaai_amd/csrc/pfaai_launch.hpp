@@ -54,7 +54,9 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
 #define PLKA(BF)                                                                                                     \
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, 3, true>), dim3(r1 - r0, gy), dim3(NT), \
                        lds, s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+        c->last_walk = gp ? PFAAI_WALK_GPOS : PFAAI_WALK_SPLITTERS;
         if (wk == 0 || abs_chunk >= 0) {
+            c->last_walk = PFAAI_WALK_SPLITTERS;
             if (bigf) PLK(true, 0); else PLK(false, 0);
         } else if constexpr (kWk1 != 0) {
             if constexpr (MODE == 0) {
@@ -179,7 +181,7 @@ constexpr int kNarrowCols = 2 * 2 * 512 - 1;
 
 inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                           hipStream_t s) {
-    if (DIAG_ENV("PFAAI_PL_NO512") || !pl_uses_ends(c, 0) || !c->copy_stream || !c->side_ev[0] || !c->side_ev[1])
+    if (DIAG_ENV("PFAAI_PL_NO512") || !pl_uses_ends(c, 0) || !c->side_stream || !c->narrow_ev[0] || !c->narrow_ev[1])
         return false;
     const int64_t n = c->prob.n_ids;  // all-vs-all: row r is genome r, n - 1 - r columns
     const int64_t cut = std::max(rb, std::min(re, n - 1 - (int64_t)kNarrowCols));
@@ -187,6 +189,7 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
     const int32_t cols_all = c->cols_run;
     if (ceil_div((int64_t)(n - 1 - cut) + 1, 2 * 2 * 512) != 1) return false;  // one chunk, or not the WK 3 form
     auto narrow = [&](hipStream_t st) {
+        c->last_narrow = true;
         c->cols_run = (int32_t)(n - 1 - cut);  // the narrow launch's widest row
         if (pick_kw<512>(c->cols_run, 2) == 1)
             launch_pl<0, 1, 512, 8, 1, true>(c, cut, re, flags, aji, S, N, st);
@@ -198,11 +201,11 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
         narrow(s);
         return true;
     }
-    // fork: the narrow rows on the second stream after everything before this
+    // fork: the narrow rows on the side stream after everything before this
     // launch on s; join: s waits for them before what follows (the run's end event)
-    if (hipEventRecord(c->side_ev[0], s) != hipSuccess || hipStreamWaitEvent(c->copy_stream, c->side_ev[0], 0) != hipSuccess)
+    if (hipEventRecord(c->narrow_ev[0], s) != hipSuccess || hipStreamWaitEvent(c->side_stream, c->narrow_ev[0], 0) != hipSuccess)
         return false;
-    narrow(c->copy_stream);
+    narrow(c->side_stream);
     switch (pick_kw<1024>(cols_all, 5)) {
         case 1: launch_pl<0, 1, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
         case 2: launch_pl<0, 2, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
@@ -210,8 +213,8 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
         case 4: launch_pl<0, 4, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
         default: launch_pl<0, 5, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
     }
-    (void)hipEventRecord(c->side_ev[1], c->copy_stream);
-    (void)hipStreamWaitEvent(s, c->side_ev[1], 0);
+    (void)hipEventRecord(c->narrow_ev[1], c->side_stream);
+    (void)hipStreamWaitEvent(s, c->narrow_ev[1], 0);
     return true;
 }
 

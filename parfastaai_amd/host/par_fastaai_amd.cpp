@@ -359,8 +359,11 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         impl.run();
         const double ms_run = ms_since(t1);
         const int rk = impl.rowsKernel();
-        std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; %s)\n", impl.nDevices(), ms_since(t0),
-                    (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?");
+        const int wf = impl.walkForm();
+        std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; %s; walk %s%s)\n", impl.nDevices(), ms_since(t0),
+                    (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?",
+                    wf == PFAAI_WALK_GPOS ? "G_pos..G_end" : wf == PFAAI_WALK_SPLITTERS ? "run table + splitters" : "-",
+                    impl.narrowLaunch() ? ", 512-thread narrow rows" : "");
         double lc = 0, lu = 0, ld = 0;
         pfaai_load_timing(impl.context(), &lc, &lu, &ld);
         const double ms_ctor = std::chrono::duration<double, std::milli>(t1 - t0).count();

@@ -21,7 +21,9 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <random>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -291,21 +293,97 @@ inline int read_genome_lists(Conn& tc, const std::string& schema, const std::str
         }
         r.gid.push_back(id_base + gid);
         r.len.push_back(nb);
-        r.tet.insert(r.tet.end(), t, t + nb);
+        r.tet.resize(r.tet.size() + nb);
+        if (nb) std::memcpy(r.tet.data() + r.tet.size() - nb, t, (std::size_t)nb * 4);  // (unaligned blob)
     });
 }
 
-// Memberships stored in `<schema>.<acc>_tetras` (the reference's F source,
-// scp_db.hpp:161-216): the sum of its blob lengths / 4.  SQLite's length()
-// of a BLOB reads the record header only.  The `<p>_genomes` path is taken
-// only when every protein's genome lists hold exactly as many entries; a
-// DB whose two orientations disagree is read through `<p>_tetras` instead,
-// so the output is the reference's either way.
-inline int64_t tetras_entries(Conn& tc, const std::string& schema, const std::string& acc, int* rc) {
-    int64_t bytes = -1;
-    *rc = tc.each("SELECT TOTAL(length(genomes)) FROM " + schema + "`" + acc + "_tetras`",
-                  [&](sqlite3_stmt* st) { bytes = (int64_t)sqlite3_column_double(st, 0); });
-    return bytes < 0 ? -1 : bytes / 4;
+
+// Exact consistency of the two orientations.  The reference builds F from
+// `<p>_tetras` (scp_db.hpp:161-216) and reads only the lengths of the
+// `<p>_genomes` blobs (scp_db.hpp:219-262); the G path builds everything
+// from `<p>_genomes`.  The two give the same output exactly when, per
+// protein, the multisets of memberships (genome, tetramer) of the two tables
+// are equal.  Both sides are folded into order-independent keyed sums of a
+// 64-bit mix of the injective code g << 32 | (p * 160000 + t), in two lanes
+// with independent per-run random seeds (a difference goes unnoticed with
+// probability ~2^-128 per protein), plus the membership counts.  A protein
+// whose two tables disagree sends the whole DB through the `<p>_tetras`
+// path, so the output is the reference's either way.
+struct MemberSum {
+    uint64_t n = 0, a = 0, b = 0;
+    bool operator==(const MemberSum& o) const { return n == o.n && a == o.a && b == o.b; }
+    bool operator!=(const MemberSum& o) const { return !(*this == o); }
+};
+
+struct MemberSeeds {
+    uint64_t a, b;
+    static MemberSeeds fresh() {
+        std::random_device rd;
+        const uint64_t t = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        return {((uint64_t)rd() << 32 ^ rd()) ^ t, ((uint64_t)rd() << 32 ^ rd()) ^ (t * 0x9E3779B97F4A7C15ull)};
+    }
+};
+
+inline uint64_t member_mix(uint64_t x) {  // splitmix64 finaliser (a bijection)
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+inline void member_add(MemberSum& m, const MemberSeeds& sd, uint32_t g, uint32_t p, uint32_t t) {
+    const uint64_t key = (uint64_t)g << 32 | (uint64_t)(p * (uint32_t)kNTetramers + t);
+    m.n += 1;
+    m.a += member_mix(sd.a ^ key);
+    m.b += member_mix(sd.b ^ key);
+}
+
+// The largest protein count whose codes p * 160000 + t fit 32 bits.
+constexpr int kMemberMaxProt = (int)(0xFFFFFFFFull / kNTetramers);
+
+// Memberships of `<schema>.<acc>_tetras` (protein index p, genome ids
+// checked against [0, n_ids_db)); *ok = false for an id or tetramer out of
+// range (the `<p>_tetras` path then reports it as the reference would).
+inline MemberSum tetras_members(Conn& tc, const std::string& schema, const std::string& acc, uint32_t p,
+                                int32_t n_ids_db, const MemberSeeds& sd, int* rc, bool* ok) {
+    MemberSum m;
+    *ok = true;
+    *rc = tc.each("SELECT tetramer, genomes FROM " + schema + "`" + acc + "_tetras`", [&](sqlite3_stmt* st) {
+        const int32_t t = sqlite3_column_int(st, 0);
+        const int nb = sqlite3_column_bytes(st, 1) / 4;
+        const auto* g = static_cast<const int32_t*>(sqlite3_column_blob(st, 1));
+        if (t < 0 || t >= kNTetramers) {
+            *ok = false;
+            return;
+        }
+        for (int j = 0; j < nb; ++j) {
+            int32_t x;
+            std::memcpy(&x, g + j, 4);  // (blob pointers need not be 4-aligned)
+            if (x < 0 || x >= n_ids_db) {
+                *ok = false;
+                return;
+            }
+            member_add(m, sd, (uint32_t)x, p, (uint32_t)t);
+        }
+    });
+    return m;
+}
+
+// The G side of the consistency sums: the lists of genomes [id_base, id_base
+// + n) (DB-local ids gid - id_base) of protein p, entries [from, to) of r.
+inline MemberSum genome_members(const ProteinLists& r, std::size_t k_from, std::size_t k_to, std::size_t off,
+                                int32_t id_base, uint32_t p, const MemberSeeds& sd) {
+    MemberSum m;
+    for (std::size_t k = k_from; k < k_to; ++k) {
+        const uint32_t g = (uint32_t)(r.gid[k] - id_base);
+        for (int32_t j = 0; j < r.len[k]; ++j) {
+            const int32_t t = r.tet[off + j];
+            member_add(m, sd, g, p, (uint32_t)(t < 0 || t >= kNTetramers ? 0xFFFFFFFFu : t));
+        }
+        off += r.len[k];
+    }
+    return m;
 }
 
 // Sort each list (a blob is normally ascending already) and check that it
@@ -365,8 +443,10 @@ inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays
     }
     const int P = (int)meta.proteinSet.size();
     const int G = (int)meta.genomeSet.size();
+    if (P > kMemberMaxProt) return -1;
     std::vector<ProteinLists> lists(P);
     std::vector<char> sets(P, 1);
+    const MemberSeeds sd = MemberSeeds::fresh();
 #pragma omp parallel
     {
         Conn tc(path);
@@ -379,12 +459,13 @@ inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays
             }
             int rc = read_genome_lists(tc, "", meta.proteinSet[p], 0, G, r);
             if (rc != SQLITE_OK) r.err = rc;
-            if (!r.err) sets[p] = normalise_lists(r);
-            if (!r.err && sets[p]) {  // both orientations hold the same number of memberships
-                const int64_t nt = tetras_entries(tc, "", meta.proteinSet[p], &rc);
-                if (rc != SQLITE_OK) r.err = rc;
-                else sets[p] = nt == (int64_t)r.tet.size();
-            }
+            if (r.err) continue;
+            // both orientations hold exactly the same memberships
+            const MemberSum mg = genome_members(r, 0, r.gid.size(), 0, 0, (uint32_t)p, sd);
+            bool ok = true;
+            const MemberSum mt = tetras_members(tc, "", meta.proteinSet[p], (uint32_t)p, G, sd, &rc, &ok);
+            if (rc != SQLITE_OK) r.err = rc;
+            else sets[p] = ok && mg == mt && normalise_lists(r);
         }
     }
     for (int p = 0; p < P; ++p)
@@ -429,8 +510,10 @@ inline int load_qt_g(const std::string& tgt, const std::string& qry, DBMetaData&
     }
     const int P = (int)meta.proteinSet.size();
     const int nT = (int)meta.genomeSet.size(), nQ = (int)meta.qyGenomeSet.size();
+    if (P > kMemberMaxProt) return -1;
     std::vector<ProteinLists> lists(P);
     std::vector<char> sets(P, 1);
+    const MemberSeeds sd = MemberSeeds::fresh();
 #pragma omp parallel
     {
         Conn tc(tgt);
@@ -443,16 +526,19 @@ inline int load_qt_g(const std::string& tgt, const std::string& qry, DBMetaData&
                 continue;
             }
             int rc = read_genome_lists(tc, "main.", meta.proteinSet[p], 0, nT, r);
-            const int64_t n_main = (int64_t)r.tet.size();
+            const std::size_t k_main = r.gid.size(), n_main = r.tet.size();
             if (rc == SQLITE_OK) rc = read_genome_lists(tc, "QueryDB.", meta.proteinSet[p], nT, nQ, r);
             if (rc != SQLITE_OK) r.err = rc;
-            if (!r.err) sets[p] = normalise_lists(r);
-            if (!r.err && sets[p]) {  // per DB: both orientations hold the same number of memberships
-                const int64_t nt_main = tetras_entries(tc, "main.", meta.proteinSet[p], &rc);
-                const int64_t nt_qry = rc == SQLITE_OK ? tetras_entries(tc, "QueryDB.", meta.proteinSet[p], &rc) : -1;
-                if (rc != SQLITE_OK) r.err = rc;
-                else sets[p] = nt_main == n_main && nt_qry == (int64_t)r.tet.size() - n_main;
-            }
+            if (r.err) continue;
+            // per DB: both orientations hold exactly the same memberships
+            const MemberSum mg_t = genome_members(r, 0, k_main, 0, 0, (uint32_t)p, sd);
+            const MemberSum mg_q = genome_members(r, k_main, r.gid.size(), n_main, nT, (uint32_t)p, sd);
+            bool ok_t = true, ok_q = true;
+            const MemberSum mt_t = tetras_members(tc, "main.", meta.proteinSet[p], (uint32_t)p, nT, sd, &rc, &ok_t);
+            MemberSum mt_q;
+            if (rc == SQLITE_OK) mt_q = tetras_members(tc, "QueryDB.", meta.proteinSet[p], (uint32_t)p, nQ, sd, &rc, &ok_q);
+            if (rc != SQLITE_OK) r.err = rc;
+            else sets[p] = ok_t && ok_q && mg_t == mt_t && mg_q == mt_q && normalise_lists(r);
         }
     }
     for (int p = 0; p < P; ++p)

@@ -40,7 +40,32 @@ CASES = {
     # J of E[0]'s protein; the drop-in CLI's default must print the same bytes
     "zero3": ("sets", dict(n_genomes=3, n_prot=2)),
     "zero30": ("sets", dict(n_genomes=30, n_prot=3)),
+    # a DB whose `<p>_genomes` blobs disagree with its `<p>_tetras` blobs at
+    # equal membership counts (mutate_equal_count): the reference reads F from
+    # `<p>_tetras` and only the lengths of `<p>_genomes` (scp_db.hpp:161-262),
+    # so a drop-in that trusted `<p>_genomes` would print other values
+    "mismatch24": ("mismatch", dict(n_genomes=24, n_prot=6, clade_size=4)),
 }
+
+
+def mutate_equal_count(db, acc="SYN00002.1", k=3):
+    """Replace one tetramer of the k-th `<acc>_genomes` blob by one the blob
+    does not hold (same length, still a sorted set): the two orientations
+    then hold equally many but different memberships."""
+    import sqlite3
+
+    import numpy as np
+
+    con = sqlite3.connect(db)
+    gid, blob = con.execute(f"SELECT genome_id, tetramers FROM `{acc}_genomes` ORDER BY genome_id LIMIT 1 OFFSET {k}"
+                            ).fetchone()
+    t = np.frombuffer(blob, "<i4").copy()
+    have = set(t.tolist())
+    t[len(t) // 2] = next(x for x in range(159999, 0, -1) if x not in have)
+    con.execute(f"UPDATE `{acc}_genomes` SET tetramers = ? WHERE genome_id = ?",
+                (np.sort(t).astype("<i4").tobytes(), gid))
+    con.commit()
+    con.close()
 
 
 def sets_for(name):
@@ -99,6 +124,11 @@ def main():
             elif kind == "sets":
                 db = os.path.join(td, name + ".db")
                 syn.write_db_sets(db, sets_for(name), **kw)
+                run_ref([db], out)
+            elif kind == "mismatch":
+                db = os.path.join(td, name + ".db")
+                syn.write_db(db, **kw)
+                mutate_equal_count(db)
                 run_ref([db], out)
             else:
                 kw = dict(kw)

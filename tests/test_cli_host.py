@@ -188,3 +188,34 @@ def test_genomes_loader_falls_back_when_orientations_disagree(tmp_path):
     con.close()
     r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", str(tmp_path / "g"))
     assert r.returncode == 0 and "<p>_tetras -> F" in r.stdout, r.stdout + r.stderr
+
+
+def test_genomes_loader_falls_back_at_equal_counts(tmp_path):
+    """Exact check, not a count: the `<p>_genomes` lists of one protein hold
+    as many memberships as its `<p>_tetras` blobs but a different one
+    (make_ref_vectors.mutate_equal_count) -> the `<p>_tetras` path (the CSV
+    against the reference binary's: tests/test_gpu_cli.py); the same for
+    the query DB of -r."""
+    import make_ref_vectors as mk
+    from parfastaai_amd import syn
+
+    _, kw = mk.CASES["mismatch24"]
+    db = str(tmp_path / "m.db")
+    syn.write_db(db, **kw)
+    r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", str(tmp_path / "g"))
+    assert r.returncode == 0 and "<p>_genomes -> G" in r.stdout, r.stdout + r.stderr
+    mk.mutate_equal_count(db)
+    r = run(db, str(tmp_path / "o.csv"), "--dump-genomes", str(tmp_path / "g"))
+    assert r.returncode == 0 and "<p>_tetras -> F" in r.stdout, r.stdout + r.stderr
+    # -r: an intact target DB with a mutated query DB, and the other way round
+    q, qm = str(tmp_path / "q.db"), str(tmp_path / "qm.db")
+    syn.write_db(q, genome_prefix="qry", **kw)
+    syn.write_db(qm, genome_prefix="qry", **kw)
+    mk.mutate_equal_count(qm)
+    t = str(tmp_path / "t.db")
+    syn.write_db(t, **kw)
+    r = run(t, str(tmp_path / "o.csv"), "-r", q, "--dump-genomes", str(tmp_path / "g"))
+    assert r.returncode == 0 and "<p>_genomes -> G" in r.stdout, r.stdout + r.stderr
+    for a, b in ((t, qm), (db, q)):
+        r = run(a, str(tmp_path / "o.csv"), "-r", b, "--dump-genomes", str(tmp_path / "g"))
+        assert r.returncode == 0 and "<p>_tetras -> F" in r.stdout, r.stdout + r.stderr

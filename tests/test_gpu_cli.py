@@ -37,8 +37,10 @@ def test_cli_csv_bytes(tmp_path, name, devs):
     db = unpack(tmp_path, name + ".db")
     out = tmp_path / "out.csv"
     r = run(db, str(out), "--bin", str(tmp_path / "o"), *devs)
-    # the drop-in runs the benchmarked path: <p>_genomes -> G, F built on the GPU, k_rows_pl
-    assert "<p>_genomes -> G" in r.stdout and "; k_rows_pl)" in r.stdout, r.stdout
+    # the drop-in runs the benchmarked path: <p>_genomes -> G, F (and G_pos / G_end) built on the GPU,
+    # k_rows_pl walking from G_pos to G_end (pfaai_run_walk), the narrow rows as the 512-thread launch
+    assert "<p>_genomes -> G" in r.stdout and "; k_rows_pl; walk G_pos..G_end, 512-thread narrow rows)" in r.stdout, \
+        r.stdout
     assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
     J = fm.read_jac(str(tmp_path / "o_jac.bin"))
     Jr = fm.read_jac(gpath(name + "_jac.bin"))
@@ -100,6 +102,27 @@ def test_cli_vs_reference_binary_on_syn(tmp_path, case, devs):
     assert open(out).read() == text(f"ref_{case}.csv")
 
 
+def test_cli_orientations_disagree_at_equal_counts(tmp_path):
+    """A DB whose `<p>_genomes` blobs hold as many but other memberships than
+    its `<p>_tetras` blobs (make_ref_vectors.mutate_equal_count): the exact
+    membership check sends it through `<p>_tetras`, and the CSV equals the
+    reference binary's on that DB (tests/golden/ref_mismatch24.csv.gz) --
+    trusting `<p>_genomes` would print other values."""
+    import make_ref_vectors as mk
+    _, kw = mk.CASES["mismatch24"]
+    db = str(tmp_path / "m.db")
+    syn.write_db(db, **kw)
+    out = tmp_path / "o.csv"
+    r = run(db, str(out))
+    assert "<p>_genomes -> G" in r.stdout
+    intact = out.read_text()
+    mk.mutate_equal_count(db)
+    r = run(db, str(out))
+    assert "<p>_tetras -> F" in r.stdout, r.stdout
+    assert out.read_text() == text("ref_mismatch24.csv")
+    assert intact == text("ref_mismatch24.csv")  # (the reference ignores the `<p>_genomes` contents)
+
+
 @pytest.mark.parametrize("name", ["xdb_subset1", "xdb_subset2"])
 def test_cli_stream_aji_equals_reference_bin(tmp_path, name):
     """--stream-aji (pfaai_stream, tiles of 7 pairs) writes the reference's
@@ -126,10 +149,10 @@ def test_cli_both_loaders_same_bytes(tmp_path, loader):
     db = unpack(tmp_path, "xdb_subset1.db")
     q = unpack(tmp_path, "xdb_subset2.db")
     r = run(db, str(tmp_path / "a.csv"), "--loader", loader)
-    assert "; k_rows_pl)" in r.stdout, r.stdout
+    assert "; k_rows_pl; walk G_pos..G_end" in r.stdout, r.stdout
     assert (tmp_path / "a.csv").read_text() == text("xdb_subset1_aji_matrix_wheader.csv")
     r = run(db, str(tmp_path / "b.csv"), "-r", q, "--loader", loader, "--ref-compat", "--bin", str(tmp_path / "b"))
-    assert "; k_rows_pl)" in r.stdout, r.stdout
+    assert "; k_rows_pl; walk run table + splitters)" in r.stdout, r.stdout
     assert np.array_equal(fm.read_vec_f64(str(tmp_path / "b_aji.bin")), fm.read_vec_f64(gpath("xdb_qt_aji.bin")))
 
 
@@ -143,7 +166,7 @@ def test_cli_c1_rebuilt_db(tmp_path, compat):
     db = rebuild_xantho(str(tmp_path))
     out = tmp_path / "o.csv"
     r = run(db, str(out), *compat)
-    assert "; k_rows_pl)" in r.stdout, r.stdout
+    assert "; k_rows_pl; walk G_pos..G_end" in r.stdout, r.stdout
     assert out.read_text() == text("xanthodb_aji_matrix_wheader.csv")
     q = tmp_path / "q.txt"
     q.write_text(text("qsub_test_input.txt"))
@@ -273,3 +296,25 @@ def test_cli_fast_exit_writes_complete_outputs(tmp_path):
     assert outs["1"] == outs["0"]
     assert all(rc == [0, 0] for k, rc in outs.items() if k not in ("0", "1"))
     assert outs["1"]["a.csv"].decode() == text("xdb_subset1_aji_matrix_wheader.csv")
+
+
+@pytest.mark.timeout(600)
+def test_cli_c2_csv_equals_reference_binary(tmp_path):
+    """Config C2 end to end (SYN 2 000 x 100 SQLite DB -> CSV, 86 MB): the
+    CLI's CSV hashes to the SHA-256 of the reference binary's CSV on the same
+    DB (tests/golden/full_digests.json "C2_cli_csv", made in the container by
+    oracle/_ref/par_fastaai.x -- the reference built from its own sources),
+    and the run takes the benchmarked kernel form."""
+    import hashlib
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "full_digests.json")) as f:
+        want = json.load(f)["C2_cli_csv"]
+    db = str(tmp_path / "c2.db")
+    syn.write_db(db, 2000, 100)
+    out = tmp_path / "c2.csv"
+    r = run(db, str(out))
+    assert "<p>_genomes -> G" in r.stdout and "; k_rows_pl; walk G_pos..G_end, 512-thread narrow rows)" in r.stdout, \
+        r.stdout
+    assert out.stat().st_size == want["bytes"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == want["sha256"]

@@ -2,13 +2,26 @@
 pinned CPU oracle (SURVEY §8d sizes; the reference itself cannot run any of
 them: |E| > 2^31, ds_helper.hpp:209,365; N >= 46 342, ds_impl.hpp:79).
 
-  C3  SYN 10 000 x 100 all-vs-all: kernel |E| == the oracle's exact count,
-      sampled rows bit-exact (S, N, AJI) against the oracle's dense
-      restatement, and the 8-way row-block split of the multi-GPU path
-      (shard.split_rows, one pfaai_run per block on this device) equal to
-      the single run bit for bit.
+  C2  SYN 2 000 x 100 all-vs-all, every input orientation (F and G, G
+      only = the CLI's load, F only = the reference's DataStructInterface):
+      the whole S / N / AJI vectors equal the oracle's (SHA-256 digests).
+  C3  SYN 10 000 x 100 all-vs-all: the whole S / N / AJI vectors (all
+      49 995 000 pairs) equal the oracle's, for the bench's load (F and G),
+      for the CLI's (G only) and for the 8-way row-block split of the
+      multi-GPU path (shard.split_rows, one pfaai_run per block); kernel |E|
+      == the oracle's exact count; sampled rows also compared value by value.
   C4  query-vs-target, 50 000 targets x 1 000 queries (the -r path, corrected
-      semantics): |E| == the oracle's count, sampled query rows bit-exact.
+      semantics): the whole output equals the oracle's; |E| == the oracle's
+      count, sampled query rows bit-exact.
+
+Whole-output digests: tests/golden/full_digests.json, written in the
+container by tests/golden/make_full_digests.py (the oracle's Appendix-A
+restatement over every row, oracle_full_rows, pinned by
+tests/test_oracle.py::test_full_rows_matches_ref).  The reference's own
+tests assert equality of the entire JAC / AJI vectors
+(pfaai_tests.cpp:355-386); these are that assertion at the benchmark sizes.
+The generated inputs' digest is compared first, so a generator difference
+between the two machines is reported as such.
   C5  SYN 100 000 x 100 all-vs-all streamed in output tiles (pfaai_stream):
       tiles arrive in order and cover every pair, 0 <= AJI <= 1 and
       1 <= N <= P everywhere, sampled rows and their |E| bit-exact against
@@ -17,6 +30,7 @@ them: |E| > 2^31, ds_helper.hpp:209,365; N >= 46 342, ds_impl.hpp:79).
 Each case prints progress to $PFAAI_PROGRESS (if set) so a long GPU call is
 never silent.
 """
+import json
 import os
 import time
 
@@ -28,6 +42,9 @@ from parfastaai_amd import _capi, syn
 from parfastaai_amd.shard import split_rows
 
 pytestmark = pytest.mark.gpu
+
+with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_digests.json")) as _f:
+    DIGESTS = json.load(_f)
 
 
 def progress(msg):
@@ -50,6 +67,25 @@ def _dev_run(engine, rb, re, n_pairs, flags=0):
     return aji, S, N
 
 
+def _assert_digests(cfg, aji, S, N, what):
+    """The device S / N / AJI vectors (whole JAC order) hash to the oracle's."""
+    import make_full_digests as mk
+
+    got = mk.output_digests(S.cpu().numpy(), N.cpu().numpy(), aji.cpu().numpy())
+    want = DIGESTS[cfg]["sha256"]
+    assert got == want, f"{cfg} {what}: {got} != {want}"
+    progress(f"{cfg} {what}: whole output equals the oracle's")
+
+
+def _problem(cfg):
+    """The config's problem as make_full_digests generated it (input digest checked)."""
+    import make_full_digests as mk
+
+    pb = mk.problem(cfg)
+    assert mk.input_digest(pb) == DIGESTS[cfg]["input_sha256"], f"{cfg}: generated inputs differ from the container's"
+    return pb
+
+
 def _check_all_rows(pr, n, rows, aji, S, N, first=0):
     """rows of an all-vs-all run (host arrays indexed by JAC index - first)
     bit-exact against the oracle's dense restatement."""
@@ -63,12 +99,23 @@ def _check_all_rows(pr, n, rows, aji, S, N, first=0):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("orient", ["both", "g_only", "f_only"])
+def test_c2_whole_output(engine, orient):
+    """C2 (SYN 2 000 x 100), every pair, in each input orientation."""
+    pb = _problem("C2")
+    drop = {"both": (), "g_only": ("Lp", "F_prot", "F_genome"), "f_only": ("G_off", "G_tet")}[orient]
+    engine.load(**{k: v for k, v in pb.items() if k not in drop})
+    _, npairs = engine.shape()
+    aji, S, N = _dev_run(engine, 0, 2000, npairs)
+    assert engine.stats()["n_events"] == DIGESTS["C2"]["events"]
+    _assert_digests("C2", aji, S, N, orient)
+
+
+@pytest.mark.timeout(300)
 def test_c3_10k_all_vs_all_and_8way_rowblocks(engine):
     n, P = 10000, 100
     t0 = time.time()
-    g = syn.generate(n, P)
-    pb = dict(mode=_capi.MODE_ALL, n_ids=n, n_prot=P, Lp=g["Lp"], F_prot=g["F_prot"], F_genome=g["F_genome"],
-              T=g["T"], G_off=g["G_off"], G_tet=g["G_tet"])
+    pb = _problem("C3")
     engine.load(**pb)
     progress(f"C3 generated + loaded in {time.time() - t0:.1f}s")
     pr = O.Problem(pb)
@@ -77,7 +124,8 @@ def test_c3_10k_all_vs_all_and_8way_rowblocks(engine):
     aji, S, N = _dev_run(engine, 0, n, npairs)
     st = engine.stats()
     assert st["rows_kernel"] == "pl"
-    assert st["n_events"] == pr.count_e()  # the reference's |E| (countTetramerTuples)
+    assert st["n_events"] == pr.count_e() == DIGESTS["C3"]["events"]  # the reference's |E| (countTetramerTuples)
+    _assert_digests("C3", aji, S, N, "F and G given (the bench's load)")
     Ah, Sh, Nh = aji.cpu().numpy(), S.cpu().numpy(), N.cpu().numpy()
     assert (Nh >= 1).all() and (Nh <= P).all()
     assert (Ah > 0).all() and (Ah <= 1).all()
@@ -98,31 +146,30 @@ def test_c3_10k_all_vs_all_and_8way_rowblocks(engine):
         ev += engine.stats()["n_events"]
     assert ev == st["n_events"]
     assert torch.equal(a8, aji) and torch.equal(S8, S) and torch.equal(N8, N)
-    progress("C3 8-way row blocks equal")
+    _assert_digests("C3", a8, S8, N8, "8-way row blocks")
+    del a8, S8, N8, aji, S, N
+    # the CLI's load: G only (`<p>_genomes`), F built on the device
+    engine.load(**{k: v for k, v in pb.items() if k not in ("Lp", "F_prot", "F_genome")})
+    assert engine.load_info() == "f_from_g"
+    aji, S, N = _dev_run(engine, 0, n, npairs)
+    _assert_digests("C3", aji, S, N, "G only (the CLI's load)")
 
 
 @pytest.mark.timeout(300)
 def test_c4_qt_50000_targets_x_1000_queries(engine):
-    nT, nQ, P, K = 50000, 1000, 100, 20
+    nT, nQ, P = 50000, 1000, 100
     t0 = time.time()
-    gt = syn.generate(nT, P, clade_size=K)
-    gq = syn.generate(nQ, P, clade_size=K, genome_seed=syn.DEFAULT_SEED + 1, n_clades=(nT + K - 1) // K,
-                      clade_mod=True)
-    m = syn.qt_merge(gt, gq)
-    del gt, gq
-    is_q = np.zeros(nT + nQ, np.uint8)
-    is_q[nT:] = 1
-    pb = dict(mode=_capi.MODE_QT, n_ids=nT + nQ, n_prot=P, n_qry=nQ, n_tgt=nT, is_q=is_q, Lp=m["Lp"],
-              F_prot=m["F_prot"], F_genome=m["F_genome"], T=m["T"], G_off=m["G_off"], G_tet=m["G_tet"])
+    pb = _problem("C4")
     engine.load(**pb)
-    progress(f"C4 generated + loaded in {time.time() - t0:.1f}s (|F| = {len(m['F_genome'])})")
+    progress(f"C4 generated + loaded in {time.time() - t0:.1f}s (|F| = {len(pb['F_genome'])})")
     pr = O.Problem(pb)
     _, npairs = engine.shape()
     assert npairs == nQ * nT
     aji, S, N = _dev_run(engine, 0, nQ, npairs)
     st = engine.stats()
     assert st["rows_kernel"] == "pl"
-    assert st["n_events"] == pr.count_e()
+    assert st["n_events"] == pr.count_e() == DIGESTS["C4"]["events"]
+    _assert_digests("C4", aji, S, N, "query-vs-target")
     Ah, Sh, Nh = aji.cpu().numpy(), S.cpu().numpy(), N.cpu().numpy()
     assert (Nh >= 0).all() and (Nh <= P).all() and (Ah >= 0).all() and (Ah <= 1).all()
     for q in (0, 1, 499, nQ - 1):

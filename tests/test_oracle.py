@@ -103,3 +103,37 @@ def test_dense_restatement_matches_ref(name):
     assert ne == r["n_events"]
     assert np.array_equal(S[ga, gb], r["S"])
     assert np.array_equal(N[ga, gb], r["N"])
+
+
+@pytest.mark.parametrize("name", ["all48", "all32_sparse", "qt12", "syn300", "qt_syn"])
+def test_full_rows_matches_ref(name):
+    """oracle_full_rows (the whole-output digests' restatement, row windows,
+    OpenMP over rows) == the E/sort restatement pinned above (correct mode),
+    in JAC order, over uneven row windows."""
+    from helpers import qt_syn
+    from parfastaai_amd import syn
+    from parfastaai_amd.datastruct import ParFAAIData
+
+    if name == "syn300":
+        g = syn.generate(300, 24, clade_size=10)
+        ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"])
+    elif name == "qt_syn":
+        ds = qt_syn(dict(n_tgt=120, n_qry=17, n_prot=12, clade_size=8))
+    else:
+        ds, _ = syn_case(name)
+    pr = O.Problem(ds.problem(), compat=False)
+    r = pr.ref_run()
+    n = pr.n_pairs()
+    S, N, A = np.full(n, -1.0), np.full(n, -1, np.int32), np.full(n, -1.0)
+    rows = pr.mode.n_ids if pr.mode.mode == 0 else pr.mode.n_qry
+    cuts = sorted({0, rows, *[min(rows, x) for x in (1, 7, rows // 3, rows // 2 + 5)]})
+    ne = 0
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        if pr.mode.mode == 0:
+            f = pr.mode.n_ids * lo - (lo + 1) * lo // 2
+            c = pr.mode.n_ids * hi - (hi + 1) * hi // 2 - f
+        else:
+            f, c = lo * pr.mode.n_tgt, (hi - lo) * pr.mode.n_tgt
+        ne += pr.full_rows(lo, hi, S[f:f + c], N[f:f + c], A[f:f + c])
+    assert ne == r["n_events"]
+    assert np.array_equal(N, r["N"]) and np.array_equal(S, r["S"]) and np.array_equal(A, r["AJI"])
