@@ -140,7 +140,9 @@ enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3, RK_V2 
 // scalars buffer layout (u64 each)
 // SC_HF / SC_HG: the both-given load's membership sums over F (k_hash_f) and
 // over G (k_gend), pfaai_sort.hpp DstGpos
-enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_HF = 5, SC_HG = 6, SC_N = 7 };
+// (second lanes SC_HF2 / SC_HG2 = SC_HF / SC_HG + 2, keyed by an independent seed)
+enum { SC_GRAND = 0, SC_FIRST_KEY = 1, SC_EVENTS = 2, SC_ERR = 3, SC_NC = 4, SC_HF = 5, SC_HG = 6, SC_HF2 = 7, SC_HG2 = 8,
+       SC_N = 9 };
 
 inline int fail(pfaai_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;

@@ -623,12 +623,12 @@ int build_g_from_f_sorted(pfaai_ctx* c, int64_t ng, int64_t n_f, int jb, bool wa
 // of the membership check (pfaai_sort.hpp, DstGpos) on the second stream
 // beside the sort.  The G side comes from k_gend (HASH), launched by
 // load_impl, which then compares the two (finish_g_check).
-int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, hipStream_t s) {
+int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, uint64_t seed2, hipStream_t s) {
     const int kb = bits_for((int64_t)c->prob.n_ids * c->prob.n_prot);
     int rc;
     if ((rc = ensure_tsort(c, n_f, kb, false))) return rc;
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 2 * sizeof(unsigned long long), s));  // SC_HF, SC_HG
+    HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));  // SC_HF, SC_HG, SC_HF2, SC_HG2
     const SrcFKeys src{static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
                        (uint32_t)c->prob.n_prot, static_cast<uint16_t*>(c->Fp16.p)};
     const DstGpos dst{gpos};
@@ -642,7 +642,7 @@ int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, 
     HIPCHK(c, hipStreamWaitEvent(c->copy_stream, ev[0], 0));
     hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->Lp.p),
                        static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
-                       (uint32_t)c->prob.n_prot, seed, sc + SC_HF);
+                       (uint32_t)c->prob.n_prot, seed, seed2, sc + SC_HF);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->copy_stream));
     rc = tsort(c, src, dst, n_f, kb, s);
@@ -673,10 +673,10 @@ int build_gpos_from_f(pfaai_ctx* c, int64_t n_f, hipStream_t s) {
 
 // After k_gend<*, true>: -1 unless the F and G membership sums agree.
 int finish_g_check(pfaai_ctx* c, hipStream_t s) {
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[4] = {0, 0, 0, 0};
     HIPCHK(c, hipMemcpyAsync(h, static_cast<unsigned long long*>(c->scalars.p) + SC_HF, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    return h[0] != h[1] ? -1 : PFAAI_RC_OK;  // [HF, HG]
+    return h[0] != h[1] || h[2] != h[3] ? -1 : PFAAI_RC_OK;  // [HF, HG, HF2, HG2]
 }
 
 // G only (the CLI's `<p>_genomes` ingest): the G entries enumerated
@@ -1006,7 +1006,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     }
     bool has_g = in_g;
     bool g_check = false;  // both given: the membership sums, completed by k_gend's G side
-    uint64_t check_seed = 0;
+    uint64_t check_seed = 0, check_seed2 = 0;
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         // both given, same size (ALL / QSUB, and QT with F's own G): G must BE
         // the transpose of F, proven by the membership sums over F (k_hash_f)
@@ -1014,16 +1014,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         // sort of F by (genome, protein).  Without G_pos no sort runs.
         check_seed = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}() ^
                      (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        check_seed2 = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}();
         g_check = true;
         if (want_pos) {
-            if ((rc = check_g_transpose(c, n_f, static_cast<uint32_t*>(c->G_pos.p), check_seed, s))) return rc;
+            if ((rc = check_g_transpose(c, n_f, static_cast<uint32_t*>(c->G_pos.p), check_seed, check_seed2, s))) return rc;
             fp16_done = true;
         } else {
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-            HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 2 * sizeof(unsigned long long), s));
+            HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));
             hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
                                static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), (uint32_t)P,
-                               check_seed, sc + SC_HF);
+                               check_seed, check_seed2, sc + SC_HF);
             HIPCHK(c, hipGetLastError());
         }
         pos_ok = true;
@@ -1129,17 +1130,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
             auto* gend = static_cast<uint32_t*>(c->G_end.p);
             if (g_check)
                 hipLaunchKernelGGL((k_gend<true, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, check_seed, sums);
+                                   gend, check_seed, check_seed2, sums);
             else
                 hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, 0ull, nullptr);
+                                   gend, 0ull, 0ull, nullptr);
             HIPCHK(c, hipGetLastError());
             d.G_end = static_cast<const uint32_t*>(c->G_end.p);
         } else {
             release(c->G_end);
             if (g_check) {
                 hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
-                                   nullptr, nullptr, check_seed, sums);
+                                   nullptr, nullptr, check_seed, check_seed2, sums);
                 HIPCHK(c, hipGetLastError());
             }
         }

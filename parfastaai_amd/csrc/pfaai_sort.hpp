@@ -114,9 +114,9 @@ struct DstRecs {
 // t order = F index order, so the sorted positions ARE G's positions.  The
 // set equality is proven by keyed hash sums: the sum over F of h(g * P + p,
 // t) (k_hash_f, streaming F block by block) must equal the sum over G of
-// h(list, G_tet) (k_gend) -- they agree for different sets with probability
-// ~2^-64 (h is a 64-bit mix of the injective 50-bit code key << 18 | t,
-// keyed by a per-load random seed).  So the sort's passes load nothing
+// h(list, G_tet) (k_gend) -- in two lanes keyed by independent per-load
+// random seeds, so different sets agree with probability ~2^-128 (h is a
+// 64-bit mix of the injective 50-bit code key << 18 | t).  So the sort's passes load nothing
 // beyond their records (the first form checked list bounds by G_off[key],
 // G_off[key + 1] and read G_tet[pos] per record in the last pass: ~3 random
 // L2 requests per record, 3.4 ms of a 10k load's pass).
@@ -145,10 +145,12 @@ struct DstGpos {
 // the F side of the membership sum: h(g * P + p, t) over every F entry of
 // every tetramer block t (one workgroup per block, grid-stride; four entries
 // per thread in flight, indices clamped rather than loads under a branch)
+// Two lanes (seed, seed2: independent per-load random keys; sums[0] and
+// sums[2]): a different multiset passes both with probability ~2^-128.
 __global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                 const int32_t* __restrict__ Fg, uint32_t P, uint64_t seed,
-                                                unsigned long long* __restrict__ sum) {
-    uint64_t acc = 0;
+                                                uint64_t seed2, unsigned long long* __restrict__ sum) {
+    uint64_t acc = 0, acc2 = 0;
     for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
         const int64_t b = Lp[t], e = Lp[t + 1];
         for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * 256) {
@@ -160,12 +162,21 @@ __global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, 
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (i0 + u * 256 < e) acc += member_hash(seed, key[u], (uint32_t)t);
+                if (i0 + u * 256 < e) {
+                    acc += member_hash(seed, key[u], (uint32_t)t);
+                    acc2 += member_hash(seed2, key[u], (uint32_t)t);
+                }
         }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sum, (unsigned long long)acc);
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_down(acc, o, 64);
+        acc2 += __shfl_down(acc2, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (acc) atomicAdd(sum, (unsigned long long)acc);
+        if (acc2) atomicAdd(sum + 2, (unsigned long long)acc2);
+    }
 }
 
 // F only (records key g * P + p | t << kb | j << (kb + 18) from k_fkeys_rec,
@@ -664,7 +675,8 @@ __global__ void k_len_from_t(const int32_t* __restrict__ T, int32_t P, int32_t n
 //         from the run-end table (k_blk_end, u32, p-major) -- looked up once
 //         per load, so the WK 3 row kernel reads (G_pos, G_end) coalesced;
 //   HASH: the G side of the both-given check (DstGpos): sums[0] +=
-//         h(list of k, G_tet[k]).
+//         h(list of k, G_tet[k]) and, keyed by seed2, sums[2] (k_hash_f's
+//         second lane).
 // The lists are taken protein-major (all genomes of protein p, then p + 1),
 // so the table lookups in flight hit one or two protein rows (640 KB each),
 // which stay in every XCD's L2 -- genome-major order touched all 100 rows at
@@ -677,7 +689,7 @@ constexpr int kGendLists = 32;
 template <bool END, bool HASH>
 __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
                                               int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
-                                              uint32_t* __restrict__ G_end, uint64_t seed,
+                                              uint32_t* __restrict__ G_end, uint64_t seed, uint64_t seed2,
                                               unsigned long long* __restrict__ sums) {
     __shared__ int64_t lb[kGendLists];
     __shared__ uint32_t pre[kGendLists + 1];
@@ -685,7 +697,7 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
     __shared__ uint32_t lid[kGendLists];
     const int tid = threadIdx.x;
     const int64_t n_ids = n_lists / P;
-    uint64_t hm = 0;
+    uint64_t hm = 0, hm2 = 0;
     for (int64_t q0 = (int64_t)blockIdx.x * kGendLists; q0 < n_lists; q0 += (int64_t)gridDim.x * kGendLists) {
         if (tid < 64) {  // one wave: the block's lists, their lengths and an inclusive scan
             uint32_t len = 0;
@@ -737,7 +749,10 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
             for (int u = 0; u < 4; ++u) {
                 if (f0 + (uint32_t)u * 256u < total) {
                     if constexpr (END) G_end[k[u]] = v[u];
-                    if constexpr (HASH) hm += member_hash(seed, li[u], (uint32_t)t[u]);
+                    if constexpr (HASH) {
+                        hm += member_hash(seed, li[u], (uint32_t)t[u]);
+                        hm2 += member_hash(seed2, li[u], (uint32_t)t[u]);
+                    }
                 }
             }
         }
@@ -745,8 +760,14 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
     }
     if constexpr (HASH) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) hm += __shfl_down(hm, o, 64);
-        if ((tid & 63) == 0 && hm) atomicAdd(&sums[0], (unsigned long long)hm);
+        for (int o = 32; o > 0; o >>= 1) {
+            hm += __shfl_down(hm, o, 64);
+            hm2 += __shfl_down(hm2, o, 64);
+        }
+        if ((tid & 63) == 0) {
+            if (hm) atomicAdd(&sums[0], (unsigned long long)hm);
+            if (hm2) atomicAdd(&sums[2], (unsigned long long)hm2);
+        }
     }
 }
 

@@ -91,11 +91,26 @@ class DataStruct:
         raise NotImplementedError
 
     def output_matrix(self, ga, gb, aji) -> np.ndarray:
-        """printOutput's dense fill (main.cpp:143-154)."""
+        """printOutput's dense fill (main.cpp:143-154).  The cell index is
+        the row-major DMatrix offset row * nT + col, as the reference's
+        unchecked operator() computes it: with the quirky -r ids and more
+        queries than targets a column can pass nT and the write lands in a
+        later row (always inside the matrix for nQ >= nT); writes happen in
+        JAC order, so the last one to a cell wins."""
         M = np.zeros((self.qrySetSize(), self.tgtSetSize()), dtype=np.float64)
-        mq = self._map_query(ga)
-        mt = self._map_target(gb)
-        M[mq, mt] = aji
+        mq = self._map_query(ga).astype(np.int64)
+        mt = self._map_target(gb).astype(np.int64)
+        flat = mq * self.tgtSetSize() + mt
+        if len(flat) and (mt.max() >= self.tgtSetSize() or flat.max() >= M.size):
+            if flat.max() >= M.size:
+                raise IndexError("output cell past the end of the matrix")
+            # last write wins: keep each cell's final JAC index
+            last = np.zeros(M.size, np.int64) - 1
+            np.maximum.at(last, flat, np.arange(len(flat)))
+            sel = last >= 0
+            M.flat[np.nonzero(sel)[0]] = np.asarray(aji)[last[sel]]
+        else:
+            M[mq, mt] = aji
         if self.is_subset_output:
             sel = self._is_qry(gb)
             M[self._map_query(gb[sel]), self._map_target(ga[sel])] = aji[sel]

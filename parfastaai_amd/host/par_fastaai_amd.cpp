@@ -330,7 +330,15 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
                         (long long)impl.nEvents(), app.streamAji.c_str());
             return rc;
         }
-        if (app.streamCsv && !app.pathToOutputFile.empty()) {  // CSV from streamed dense row tiles
+        // the reference's QT rows overlap when nQ > nT (its column placement,
+        // ds_impl.hpp:434-436 + main.cpp:149, writes later rows over earlier
+        // ones): pfaai_stream_matrix cannot reproduce that tile by tile, so
+        // such a run takes the dense writer below (same bytes)
+        const bool stream_ok = !(mode == PFAAI_MODE_QT && app.refCompat && ds.qrySetSize() > ds.tgtSetSize());
+        if (app.streamCsv && !stream_ok)
+            std::printf("--stream-csv: -r with more query than target genomes reproduces the reference's overlapping "
+                        "rows only through the dense writer; writing the CSV that way\n");
+        if (app.streamCsv && stream_ok && !app.pathToOutputFile.empty()) {  // CSV from streamed dense row tiles
             auto t1 = std::chrono::steady_clock::now();
             std::printf("Writing output with %lld query genomes and %lld target genomes. \n",
                         (long long)ds.qrySetSize(), (long long)ds.tgtSetSize());

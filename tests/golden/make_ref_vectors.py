@@ -35,6 +35,10 @@ CASES = {
     # reference's column map intact; its T-index quirk is reproduced under
     # ref-compat and pinned here)
     "qt12": ("qt", dict(n_tgt=12, n_qry=12, n_prot=20, clade_size=4)),
+    # -r with more queries than targets: the reference's rows overlap (its
+    # column placement of the quirky JAC ids, ds_impl.hpp:434-436 +
+    # main.cpp:149) -- --stream-csv must still print these bytes
+    "qt8x12": ("qt", dict(n_tgt=8, n_qry=12, n_prot=20, clade_size=4)),
     # explicit memberships (syn.write_db_sets) with pairs that share no
     # tetramer in any protein: the reference gives them the
     # J of E[0]'s protein; the drop-in CLI's default must print the same bytes

@@ -72,7 +72,7 @@ def test_cli_qt_correct_equals_merged_db_block(tmp_path):
 
 
 @pytest.mark.parametrize("devs", [[], ["--devices", "0,0,0"]], ids=["1dev", "3ctx"])
-@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12"])
+@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12", "qt8x12"])
 def test_cli_vs_reference_binary_on_syn(tmp_path, case, devs):
     """The CLI's CSV equals the reference binary's, on one context and with the
     rows split over three contexts (--devices 0,0,0: the multi-GPU path, one
@@ -185,7 +185,7 @@ def test_cli_stream_csv_bytes(tmp_path, name):
     assert out.read_text() == text(name + "_aji_matrix_wheader.csv")
 
 
-@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12"])
+@pytest.mark.parametrize("case", ["all48", "qsub40", "qt12", "qt8x12"])
 def test_cli_stream_csv_vs_reference_binary_on_syn(tmp_path, case):
     import make_ref_vectors as mk
     kind, kw = mk.CASES[case]

@@ -82,7 +82,7 @@ def test_oracle_xantho_csv_bytes():
     assert fm.csv_text(ds.refQuerySet(), ds.refTargetSet(), M) == text("xanthodb_aji_matrix_wheader.csv")
 
 
-@pytest.mark.parametrize("name", ["all48", "all32_sparse", "qsub40", "qt12"])
+@pytest.mark.parametrize("name", ["all48", "all32_sparse", "qsub40", "qt12", "qt8x12"])
 def test_oracle_vs_reference_binary(name):
     ds, M_ref = syn_case(name)
     compat = name.startswith("qt")
