@@ -352,8 +352,12 @@ def main():
     if not args.f_only:  # the DB's genome-major <p>_genomes lists: the row kernel walks them
         ds.with_genome_major(g["G_off"], g["G_tet"])
     eng = _capi.Engine(local)
+    # a rank loads the whole input but builds the walk data (G_pos / G_end,
+    # the run-end sort) of its own row block only (pfaai_load_rows); all-vs-all
+    # rows are genomes, so the blocks are known before the load
+    blocks = split_rows(args.genomes, world)
     t0 = time.perf_counter()
-    eng.load(**ds.problem())
+    eng.load(**ds.problem(), rows=blocks[rank] if world > 1 else None)
     load_wall_ms = (time.perf_counter() - t0) * 1e3
     del g
     ms_checks, ms_upload, ms_load_dev = eng.load_timing()
@@ -361,7 +365,7 @@ def main():
     log(f"pfaai_load {load_wall_ms:.0f} ms (host checks {ms_checks:.0f}, H2D {ms_upload:.0f}, device {load_path} "
         f"{ms_load_dev:.2f} ms)")
     n_rows, n_pairs = eng.shape()
-    blocks = split_rows(n_rows, world)
+    assert n_rows == args.genomes
     spans = [eng.row_span(rb, re) for rb, re in blocks]
     rb, re = blocks[rank]
     first, count = spans[rank]
@@ -441,13 +445,14 @@ def main():
         ev = torch.tensor([n_events], dtype=torch.int64, device=hdev)
         dist.all_reduce(ev)
         total_events = int(ev.item())
-        km = torch.tensor([ms_rows / max(n_runs, 1), ms_build / max(n_runs, 1), ms_load_dev + first_step_ms],
-                          dtype=torch.float64, device=hdev)
+        km = torch.tensor([ms_rows / max(n_runs, 1), ms_build / max(n_runs, 1), ms_load_dev + first_step_ms,
+                           ms_load_dev], dtype=torch.float64, device=hdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        k_rows_ms_max, k_build_ms_max, one_shot_ms = km.tolist()
+        k_rows_ms_max, k_build_ms_max, one_shot_ms, load_ms_max = km.tolist()
     else:
         total_events = n_events
         one_shot_ms = ms_load_dev + first_step_ms
+        load_ms_max = ms_load_dev
         k_rows_ms_max = ms_rows / max(n_runs, 1)
         k_build_ms_max = ms_build / max(n_runs, 1)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -458,6 +463,7 @@ def main():
         vmin, vmax = float(vals.min().item()), float(vals.max().item())
         assert vals.numel() == n_pairs and 0.0 <= vmin and vmax <= 1.0, (vals.numel(), vmin, vmax)
         if world > 1:  # the gathered row blocks equal one run over all rows on this device, bit for bit
+            eng.load(**ds.problem())  # (the whole input's walk data: this rank loaded its block only)
             full = torch.empty(n_pairs, dtype=torch.float64, device=dev)
             eng.run(0, n_rows, 0, full.data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
@@ -507,11 +513,12 @@ def main():
         # the two-pass sort moves ~50 B (pfaai_sort.hpp: per pass a histogram
         # read + a read and a write of 8-B records)
         alg_per_f = {"g_checked": 22, "g_from_f": 26, "f_from_g": 22}.get(load_path)
-        # the bytes the implemented passes move per F entry (G_CHECKED): hist 1
-        # reads F 8 + writes the u16 column 2; scatter 1 reads 8, writes 8;
-        # hist 2 reads 8; scatter 2 reads 8, writes G_pos 4; k_gend reads
-        # G_tet 4 + a 4-B run end, writes G_end 4; k_hash_f reads F 8 = 66 B
-        pass_per_f = {"g_checked": 66}.get(load_path)
+        # the bytes the implemented passes move per F entry (G_CHECKED, the
+        # run-end sort): hist 1 reads F 8 + writes the u16 column 2; scatter 1
+        # reads F 8, writes a record 8; hist 2 reads 8; scatter 2 reads 8,
+        # writes G_pos 4 + G_end 4; beside them k_hash_f reads F 8 and the G
+        # side of the check G_tet 4 = 62 B
+        pass_per_f = {"g_checked": 62}.get(load_path) if world == 1 else None
         load = {"path": load_path, "device_ms": round(ms_load_dev, 3), "host_checks_ms": round(ms_checks, 1),
                 "h2d_ms": round(ms_upload, 1), "wall_ms": round(load_wall_ms, 1), "F": n_f,
                 "alg_bytes_per_F": alg_per_f,
@@ -519,6 +526,8 @@ def main():
                 "frac": round(alg_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if alg_per_f else None,
                 "pass_bytes_per_F": pass_per_f,
                 "pass_frac": round(pass_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pass_per_f else None,
+                "device_ms_max_rank": round(load_ms_max, 3),
+                "rows": f"rank 0 of {world}: walk data of rows {list(blocks[rank])}" if world > 1 else "all",
                 "one_shot_ms": round(ms_load_dev + first_step_ms, 3), "first_step_ms": round(first_step_ms, 3),
                 "one_shot_wall_ms": round(first_wall_ms, 1)}
         cpu = None

@@ -129,6 +129,15 @@ const char* pfaai_last_error(const pfaai_ctx* ctx);
  * 75-79).  Replaces any previously loaded problem. */
 int pfaai_load(pfaai_ctx* ctx, const pfaai_problem* prob);
 
+/* pfaai_load for a context that will run only output rows [row_begin,
+ * row_end) -- one rank of a row-block partition (the reference's
+ * distributeGenomePairs, algorithm_impl.hpp:100-120).  The whole problem is
+ * loaded; the per-entry walk data of all-vs-all rows (G_pos, G_end) is built
+ * for those rows' genomes only, so a rank's load sorts and writes ~1/N of it.
+ * Rows outside the block still run (through the run table: correct, slower).
+ * Other modes: as pfaai_load. */
+int pfaai_load_rows(pfaai_ctx* ctx, const pfaai_problem* prob, int64_t row_begin, int64_t row_end);
+
 /* F construction on the device (replaces DataStructHelper::constructLc /
  * constructF / constructT, ds_helper.hpp:46-162, and the SQL UNION ALL +
  * ORDER BY of SQLiteSCPDataBase::proteinSetGPPairs, scp_db.hpp:161-216).

@@ -37,7 +37,7 @@ EXPORTS = [
     "pfaai_shape", "pfaai_row_span", "pfaai_run", "pfaai_compute", "pfaai_last_stats",
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
-    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_timing", "pfaai_stream_matrix",
+    "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_rows", "pfaai_load_timing", "pfaai_stream_matrix",
     "pfaai_load_info",
 ]
 LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
@@ -92,6 +92,7 @@ def load_library(path=None):
         "pfaai_destroy": (ctypes.c_int, [vp]),
         "pfaai_last_error": (ctypes.c_char_p, [vp]),
         "pfaai_load": (ctypes.c_int, [vp, ctypes.POINTER(Problem)]),
+        "pfaai_load_rows": (ctypes.c_int, [vp, ctypes.POINTER(Problem), i64, i64]),
         "pfaai_shape": (ctypes.c_int, [vp, P64, P64]),
         "pfaai_row_span": (ctypes.c_int, [vp, i64, i64, P64, P64]),
         "pfaai_run": (ctypes.c_int, [vp, i64, i64, u32, vp, vp, vp, vp]),
@@ -157,9 +158,11 @@ class Engine:
 
     # -- problem ----------------------------------------------------------------
     def load(self, *, mode, n_ids, n_prot, T, Lp=None, F_prot=None, F_genome=None, n_qry=0, n_tgt=0,
-             is_q=None, q_index=None, t_rank=None, G_off=None, G_tet=None):
+             is_q=None, q_index=None, t_rank=None, G_off=None, G_tet=None, rows=None):
         """F (Lp, F_prot, F_genome) and/or G (G_off, G_tet): whichever is
-        missing is built on the device (pfaai_load)."""
+        missing is built on the device (pfaai_load).  rows=(begin, end): the
+        output rows this context will run (pfaai_load_rows: a rank's block;
+        the all-vs-all walk data is built for those rows only)."""
         Lp = None if Lp is None else np.ascontiguousarray(Lp, dtype=np.int64)
         F_prot = None if F_prot is None else np.ascontiguousarray(F_prot, dtype=np.int32)
         F_genome = None if F_genome is None else np.ascontiguousarray(F_genome, dtype=np.int32)
@@ -175,7 +178,11 @@ class Engine:
                      n_tgt=n_tgt, n_f=0 if F_prot is None else F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
                      F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
                      t_rank=_ptr(t_rank), G_off=_ptr(G_off), G_tet=_ptr(G_tet))
-        self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
+        if rows is None:
+            self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
+        else:
+            self._check(self.lib.pfaai_load_rows(self.ctx, ctypes.byref(pb), int(rows[0]), int(rows[1])),
+                        "pfaai_load_rows")
 
     def shape(self):
         r, p = ctypes.c_int64(), ctypes.c_int64()

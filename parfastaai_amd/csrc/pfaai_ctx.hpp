@@ -78,6 +78,16 @@ struct pfaai_ctx {
     DevBuf rowptr, lens, key_c, rec_c, key_a, key_b, val_a, val_b, hist, hoff, recs, sums, scalars;
     DevBuf out_aji, out_S, out_N, dbg;
     DevBuf srec_a, srec_b, shist, sgsum, sbase;  // the load-time transposition sort (pfaai_sort.hpp)
+    DevBuf tails;  // the run-end sort's block-end bitmap and per-tile tables
+    DevBuf ranks;  // the run-end sort's check: block ends before each tile, tetramer ranks (u64)
+    // all-vs-all rows whose walk data (G_pos, G_end) the last load built:
+    // genomes [pos_lo, pos_hi) (pfaai_load_rows; pfaai_load: all)
+    int32_t pos_lo = 0, pos_hi = 0;
+    // the genomes whose caller-given G lists the load verified against F (a
+    // both-given pfaai_load_rows checks its block only): rows beyond them
+    // are refused, since every walk reads the row genome's G lists
+    int32_t chk_lo = 0, chk_hi = 0;
+    int64_t run_rb = 0, run_re = 0;  // rows of the current pfaai_run (pl_uses_ends)
     hipEvent_t load_ev[2] = {nullptr, nullptr};  // device span of the last load's F / G build
     hipEvent_t side_ev[2] = {nullptr, nullptr};  // the load's fork to / join from copy_stream (k_hash_f)
     // the narrow all-vs-all rows' launch beside the wide rows (launch_narrow):
@@ -217,6 +227,7 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
 // table build (run_mode) and the kernel choice (launch_pl).
 inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
     return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pos && !c->windows &&
+           c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
            !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");
 }

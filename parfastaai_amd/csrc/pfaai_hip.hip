@@ -265,6 +265,10 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     HIPCHK(c, hipMemsetAsync(sc + SC_EVENTS, 0, sizeof(unsigned long long), s));
     const bool wl = c->rows_kernel == RK_WORKLIST;
+    if (c->prob.mode == PFAAI_MODE_ALL && (rb < c->chk_lo || re > c->chk_hi))
+        return fail(c, PFAAI_RC_INVALID, "rows outside the block whose G lists pfaai_load_rows verified");
+    c->run_rb = rb;  // (pl_uses_ends: the rows' G_pos / G_end must have been built)
+    c->run_re = re;
     c->last_walk = PFAAI_WALK_NONE;  // (set by launch_pl / launch_narrow)
     c->last_narrow = false;
     // rows wider than one k_rows_pl chunk: absolute column windows, each with
@@ -580,7 +584,7 @@ int tsort(pfaai_ctx* c, const S0& src0, const DN& dstN, int64_t n, int kb, hipSt
 }
 
 void release_tsort(pfaai_ctx* c) {
-    for (DevBuf* b : {&c->srec_a, &c->srec_b, &c->shist, &c->sgsum, &c->sbase}) release(*b);
+    for (DevBuf* b : {&c->srec_a, &c->srec_b, &c->shist, &c->sgsum, &c->sbase, &c->tails, &c->ranks}) release(*b);
 }
 
 // F only: G_off from T, records (k_fkeys_rec: key, tetramer, block offset)
@@ -642,7 +646,7 @@ int check_g_transpose(pfaai_ctx* c, int64_t n_f, uint32_t* gpos, uint64_t seed, 
     HIPCHK(c, hipStreamWaitEvent(c->copy_stream, ev[0], 0));
     hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->Lp.p),
                        static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p),
-                       (uint32_t)c->prob.n_prot, seed, seed2, sc + SC_HF);
+                       (uint32_t)c->prob.n_prot, seed, seed2, sc + SC_HF, 0, c->prob.n_ids);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(ev[1], c->copy_stream));
     rc = tsort(c, src, dst, n_f, kb, s);
@@ -669,6 +673,149 @@ int build_gpos_from_f(pfaai_ctx* c, int64_t n_f, hipStream_t s) {
                        (uint32_t)c->prob.n_prot, nullptr};
     const DstGpos dst{static_cast<uint32_t*>(c->G_pos.p)};
     return tsort(c, src, dst, n_f, kb, s);
+}
+
+// All-vs-all G_pos and G_end of the lists of genomes [g_lo, g_hi) (G index
+// gbase.., n_kept entries) by the F -> G sort that carries run ends
+// (pfaai_sort.hpp: k_block_ends, k_fends_hist writes each entry's distance to
+// its run end, SrcFEnds / DstRecsEnds / DstGposEnds): two passes over F and no
+// run-end table or per-entry lookup.  check (seeds): the both-given
+// membership sums of those genomes (F side k_hash_f, G side k_gend HASH) run
+// on the second stream beside the scatters.  Returns -1 where the records do
+// not fit two passes (the caller takes check_g_transpose / the plain G_pos
+// sort + k_blk_end + k_gend).
+template <int DB>
+int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_hi, int64_t gbase, int64_t n_kept,
+                     const uint64_t* seeds, hipStream_t s) {
+    constexpr int NT = kSortNT;
+    static_assert(sort_tile<NT>() == kEndsTile, "the run-end tiles are the sort's tiles");
+    const int32_t P = c->prob.n_prot;
+    const int hb = kb - DB;
+    const int64_t kT = sort_tile<NT>(), ntiles = ceil_div(n_f, kT), ngroups = ceil_div(ntiles, kSortGroup);
+    auto* hist = static_cast<uint32_t*>(c->shist.p);
+    auto* gsum = static_cast<uint32_t*>(c->sgsum.p);
+    auto* base = static_cast<uint32_t*>(c->sbase.p);
+    uint32_t* tctr = base + (1 << DB);
+    auto* bend = static_cast<uint32_t*>(c->tails.p);
+    const int64_t nwords = ceil_div(n_f, 32);
+    uint32_t* ftail = bend + nwords;
+    uint32_t* ntail = ftail + ntiles;
+    uint32_t* ltail = ntail + ntiles;
+    uint32_t* tcnt = ltail + ntiles;   // block ends per tile (the check's ranks)
+    uint32_t* flag = tcnt + ntiles;    // non-empty tetramer blocks, then their ranks (k_gend's lookups)
+    auto* trank = static_cast<unsigned long long*>(c->ranks.p);  // [ntiles + 1]
+    unsigned long long* rho = trank + ntiles + 1;                // [160001]
+    unsigned long long* hpart = rho + kNTetramers + 1;           // [2 * ntiles]: the F side's per-tile sums
+    auto* D = static_cast<uint32_t*>(c->srec_b.p);
+    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
+    const auto* Lp = static_cast<const int64_t*>(c->Lp.p);
+    const auto* Fp = static_cast<const int32_t*>(c->Fp.p);
+    const auto* Fg = static_cast<const int32_t*>(c->Fg.p);
+    HIPCHK(c, hipMemsetAsync(bend, 0, nwords * 4, s));
+    if (seeds) HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_block_ends, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, Lp, bend);
+    if (seeds) {  // the check's tetramer ranks (pfaai_sort.hpp k_tile_ends / k_nonempty)
+        hipLaunchKernelGGL(k_tile_ends, dim3((int)std::min<int64_t>(ceil_div(ntiles, 256), 4096)), dim3(256), 0, s, bend,
+                           n_f, ntiles, tcnt);
+        hipLaunchKernelGGL(k_nonempty, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, Lp, flag);
+        int rc;
+        if ((rc = scan_u32(c, tcnt, ntiles, trank, s)) || (rc = scan_u32(c, flag, kNTetramers, rho, s))) return rc;
+        hipLaunchKernelGGL(k_rank_table, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, rho, flag);
+    }
+    const uint32_t mask1 = (1u << DB) - 1u, mask2 = (1u << hb) - 1u;
+    hipLaunchKernelGGL((k_fends_hist<DB, NT>), dim3(ntiles), dim3(NT), 0, s, Fp, Fg, bend, n_f, (uint32_t)P, g_lo, g_hi,
+                       mask1, static_cast<uint16_t*>(c->Fp16.p), D, hist, ftail, ltail, trank,
+                       seeds ? seeds[0] : 0ull, seeds ? seeds[1] : 0ull, seeds ? hpart : nullptr);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_tail_suffix, dim3(1), dim3(1024), 0, s, ftail, ntiles, ntail);
+    hipLaunchKernelGGL(k_fix_open, dim3((int)std::min<int64_t>(ceil_div(ntiles, 4), 65536)), dim3(256), 0, s, ltail, ntail,
+                       ntiles, n_f, D);
+    hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
+    hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base, tctr);
+    if (seeds) {  // the sums of the check beside the scatters: the F side's tiles, the G side
+        HIPCHK(c, hipEventRecord(c->side_ev[0], s));
+        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->side_ev[0], 0));
+        hipLaunchKernelGGL(k_sum_pairs, dim3(256), dim3(256), 0, c->copy_stream, hpart, ntiles, sc + SC_HF);
+        hipLaunchKernelGGL(k_hash_g, dim3(2048), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->G_off.p),
+                           static_cast<const int32_t*>(c->G_tet.p), P, g_lo, g_hi, flag, seeds[0], seeds[1],
+                           sc + SC_HG);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->side_ev[1], c->copy_stream));
+    }
+    const size_t lds = sort_scatter_lds<DB, NT>();
+    int cus = 256, per1 = 1, per2 = 1;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per1, reinterpret_cast<const void*>(&k_sort_scatter<DB, NT, kSortPF, SrcFEnds, DstRecsEnds>), NT, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per2, reinterpret_cast<const void*>(&k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>), NT, lds);
+    auto* rec = static_cast<uint64_t*>(c->srec_a.p);
+    const SrcFEnds src{Fp, Fg, D, (uint32_t)P, kb, g_lo, g_hi};
+    hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcFEnds, DstRecsEnds>),
+                       dim3((int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per1))), dim3(NT), lds, s, src,
+                       DstRecsEnds{rec, kb, DB}, n_f, ntiles, 0, mask1, hist, gsum, base, tctr);
+    HIPCHK(c, hipGetLastError());
+    if (n_kept > 0) {
+        const int64_t nt2 = ceil_div(n_kept, kT), ng2 = ceil_div(nt2, kSortGroup);
+        const SrcRecs src2{rec};
+        hipLaunchKernelGGL((k_sort_hist<DB, NT, SrcRecs>), dim3(nt2), dim3(NT), 0, s, src2, n_kept, 0, mask2, hist);
+        hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ng2), dim3(kSortThreads), 0, s, hist, nt2, gsum);
+        hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ng2, base, tctr);
+        hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>),
+                           dim3((int)std::min<int64_t>(nt2, (int64_t)cus * std::max(1, per2))), dim3(NT), lds, s, src2,
+                           DstGposEnds{static_cast<uint32_t*>(c->G_pos.p) + gbase, static_cast<uint32_t*>(c->G_end.p) + gbase,
+                                       hb},
+                           n_kept, nt2, 0, mask2, hist, gsum, base, tctr);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PFAAI_RC_OK;
+}
+
+// the run-end sort's buffers: records (srec_a), run-end distances (srec_b,
+// u32), the block-end bitmap + per-tile run ends (tails), tile histograms
+int ensure_gpos_ends(pfaai_ctx* c, int64_t n_f, int64_t n_kept, int db) {
+    const int64_t ntiles = ceil_div(std::max<int64_t>(n_f, 1), sort_tile<kSortNT>());
+    int rc;
+    if ((rc = ensure(c, c->srec_a, (size_t)std::max<int64_t>(n_kept, 1) * 8)) ||
+        (rc = ensure(c, c->srec_b, (size_t)std::max<int64_t>(n_f, 1) * 4)) ||
+        (rc = ensure(c, c->shist, (size_t)ntiles * (4u << db))) ||
+        (rc = ensure(c, c->sgsum, (size_t)ceil_div(ntiles, kSortGroup) * (4u << db))) ||
+        (rc = ensure(c, c->sbase, (4u << db) + 64)) ||
+        (rc = ensure(c, c->tails, (size_t)(ceil_div(std::max<int64_t>(n_f, 1), 32) + 4 * ntiles + kNTetramers) * 4)) ||
+        (rc = ensure(c, c->ranks, (size_t)(ntiles + 1 + kNTetramers + 1 + 2 * ntiles) * 8)) ||
+        (rc = ensure_scan(c, std::max<int64_t>(ntiles, kNTetramers))))
+        return rc;
+    return PFAAI_RC_OK;
+}
+
+int build_gpos_ends(pfaai_ctx* c, int64_t n_f, int32_t g_lo, int32_t g_hi, int64_t gbase, int64_t n_kept,
+                    const uint64_t* seeds, hipStream_t s) {
+    const int32_t P = c->prob.n_prot;
+    const int kb = bits_for((int64_t)c->prob.n_ids * P);
+    int passes;
+    const int db = tsort_db(kb, &passes);
+    if (passes != 2 || kb + 33 > 63 || db < 8 || db > 11 || n_f == 0) return -1;
+    int rc;
+    if ((rc = ensure_gpos_ends(c, n_f, n_kept, db))) return rc;
+    if (seeds && !c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    switch (db) {
+        case 8: rc = gpos_ends_passes<8>(c, n_f, kb, g_lo, g_hi, gbase, n_kept, seeds, s); break;
+        case 9: rc = gpos_ends_passes<9>(c, n_f, kb, g_lo, g_hi, gbase, n_kept, seeds, s); break;
+        case 10: rc = gpos_ends_passes<10>(c, n_f, kb, g_lo, g_hi, gbase, n_kept, seeds, s); break;
+        default: rc = gpos_ends_passes<11>(c, n_f, kb, g_lo, g_hi, gbase, n_kept, seeds, s); break;
+    }
+    if (seeds) {  // join (also on failure: nothing may overtake the sums on copy_stream)
+        const hipError_t we = hipStreamWaitEvent(s, c->side_ev[1], 0);
+        if (!rc && we != hipSuccess) return hip_fail(c, we, "hipStreamWaitEvent");
+    }
+    return rc;
+}
+
+// (before the load's device span: allocation inside it leaves the stream idle)
+int ensure_gpos_ends_pre(pfaai_ctx* c, int64_t n_f, int64_t n_kept, int64_t ng) {
+    int passes;
+    const int db = tsort_db(bits_for(ng), &passes);
+    return passes == 2 && db >= 8 && db <= 11 ? ensure_gpos_ends(c, n_f, n_kept, db) : PFAAI_RC_OK;
 }
 
 // After k_gend<*, true>: -1 unless the F and G membership sums agree.
@@ -720,7 +867,9 @@ int build_f_from_g_sorted(pfaai_ctx* c, int64_t n_lists, int64_t n, hipStream_t 
     return PFAAI_RC_OK;
 }
 
-int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
+// rows_lo / rows_hi: the all-vs-all rows (genomes) whose walk data (G_pos,
+// G_end) the load builds, [0, n_ids) by default (pfaai_load_rows).
+int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_t rows_hi = -1) {
     HIPCHK(c, hipSetDevice(c->device));
     c->loaded = false;
     using clk = std::chrono::steady_clock;
@@ -967,6 +1116,12 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         release(c->G_pos);
     }
     const bool want_pos = c->G_pos.p != nullptr;
+    // the rows (genomes) whose G_pos / G_end are built: a rank's block (pfaai_load_rows)
+    if (rows_hi < 0 || rows_hi > ni) rows_hi = ni;
+    rows_lo = std::max<int64_t>(0, std::min<int64_t>(rows_lo, rows_hi));
+    const int32_t g_lo = (int32_t)rows_lo, g_hi = (int32_t)rows_hi;
+    const int64_t gbase = in_g ? p.G_off[(int64_t)g_lo * P] : 0, n_kept = in_g ? p.G_off[(int64_t)g_hi * P] - gbase : 0;
+    bool ends_built = false;  // G_pos and G_end of [g_lo, g_hi) by the run-end sort (build_gpos_ends)
     // the u16 protein column (k_blk's run detection): written by the
     // transposition sorts on the way, else by k_fp16 below
     if ((rc = ensure(c, c->Fp16, (n_f + 16) * sizeof(uint16_t)))) return rc;  // 16-B reads may pass the end
@@ -977,11 +1132,13 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
         if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if (want_pos && (rc = ensure_gpos_ends_pre(c, n_f, n_kept, ng))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     } else if (in_g && !in_f && n_f && P < kMaxRuns && ng < ((int64_t)1 << 32)) {  // G only: both sorts' buffers
         if ((rc = ensure_tsort(c, n_f, 18, true))) return rc;
         if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
         if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if (want_pos && (rc = ensure_gpos_ends_pre(c, n_f, n_kept, ng))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     }
     for (hipEvent_t& e : c->load_ev)
@@ -994,8 +1151,12 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
             if ((rc = build_f_from_g_sorted(c, ng, n_f, s))) return rc;
             fp16_done = true;
             c->load_path = PFAAI_LOAD_F_FROM_G;
-            if (want_pos && ng < ((int64_t)1 << 32)) {  // the WK 3 walks' G_pos (G_end follows below)
-                if ((rc = build_gpos_from_f(c, n_f, s))) return rc;
+            if (want_pos && ng < ((int64_t)1 << 32)) {  // the WK 3 walks' G_pos and G_end
+                if (!(c->G_end.p) && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+                rc = build_gpos_ends(c, n_f, g_lo, g_hi, gbase, n_kept, nullptr, s);
+                ends_built = rc == PFAAI_RC_OK;
+                if (rc == -1 && (rc = build_gpos_from_f(c, n_f, s))) return rc;  // (G_end from k_gend below)
+                if (rc) return rc;
                 pos_ok = true;
             }
         } else {
@@ -1017,14 +1178,20 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         check_seed2 = ((uint64_t)std::random_device{}() << 32) ^ (uint64_t)std::random_device{}();
         g_check = true;
         if (want_pos) {
-            if ((rc = check_g_transpose(c, n_f, static_cast<uint32_t*>(c->G_pos.p), check_seed, check_seed2, s))) return rc;
+            const uint64_t seeds[2] = {check_seed, check_seed2};
+            rc = build_gpos_ends(c, n_f, g_lo, g_hi, gbase, n_kept, seeds, s);
+            ends_built = rc == PFAAI_RC_OK;
+            if (rc == -1 &&
+                (rc = check_g_transpose(c, n_f, static_cast<uint32_t*>(c->G_pos.p), check_seed, check_seed2, s)))
+                return rc;
+            if (rc) return rc;
             fp16_done = true;
         } else {
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
             HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));
             hipLaunchKernelGGL(k_hash_f, dim3(8192), dim3(256), 0, s, static_cast<const int64_t*>(c->Lp.p),
                                static_cast<const int32_t*>(c->Fp.p), static_cast<const int32_t*>(c->Fg.p), (uint32_t)P,
-                               check_seed, check_seed2, sc + SC_HF);
+                               check_seed, check_seed2, sc + SC_HF, 0, ni);
             HIPCHK(c, hipGetLastError());
         }
         pos_ok = true;
@@ -1112,35 +1279,37 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
     d.Fp16 = static_cast<const uint16_t*>(c->Fp16.p);
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
     d.T16c = c->T16c.p ? static_cast<const uint16_t*>(c->T16c.p) : d.T16;
-    // G_end with G_pos: the end of the F run of every G entry, from the
-    // run-end table looked up once here (k_blk_end + k_gend).  The WK 3 row
-    // kernel then reads (G_pos, G_end) of its G entries with coalesced loads
-    // instead of one run-table lookup per entry and step, and its steps build
-    // no run table.
+    // G_end with G_pos: the end of the F run of every G entry -- carried by
+    // the run-end sort (build_gpos_ends), else from the run-end table looked
+    // up once here (k_blk_end + k_gend).  The WK 3 row kernel then reads
+    // (G_pos, G_end) of its G entries with coalesced loads instead of one
+    // run-table lookup per entry and step, and its steps build no run table.
     d.G_end = nullptr;
     c->runs_valid = false;
     {
         // k_gend: G_end (with G_pos) and / or the G sides of the both-given check
         const int ggrid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, kGendLists), 1), 1 << 16);
         auto* sums = static_cast<unsigned long long*>(c->scalars.p) + SC_HG;
-        if (d.G_pos) {
+        if (d.G_pos && ends_built) {  // G_end came with G_pos; the G side of the check ran beside the sort
+            d.G_end = static_cast<const uint32_t*>(c->G_end.p);
+        } else if (d.G_pos) {
             if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
             if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
             const auto* ends = reinterpret_cast<const uint32_t*>(c->blk.p);
             auto* gend = static_cast<uint32_t*>(c->G_end.p);
             if (g_check)
                 hipLaunchKernelGGL((k_gend<true, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, check_seed, check_seed2, sums);
+                                   gend, check_seed, check_seed2, sums, 0, ni, nullptr);
             else
                 hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, 0ull, 0ull, nullptr);
+                                   gend, 0ull, 0ull, nullptr, 0, ni, nullptr);
             HIPCHK(c, hipGetLastError());
             d.G_end = static_cast<const uint32_t*>(c->G_end.p);
         } else {
             release(c->G_end);
             if (g_check) {
                 hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
-                                   nullptr, nullptr, check_seed, check_seed2, sums);
+                                   nullptr, nullptr, check_seed, check_seed2, sums, 0, ni, nullptr);
                 HIPCHK(c, hipGetLastError());
             }
         }
@@ -1152,6 +1321,11 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb) {
         }
     }
     HIPCHK(c, hipEventRecord(c->load_ev[1], s));
+    // the rows whose G_pos / G_end exist (the WK 3 walks; others take the run table)
+    c->pos_lo = ends_built ? g_lo : 0;
+    c->pos_hi = ends_built ? g_hi : ni;
+    c->chk_lo = ends_built && g_check ? g_lo : 0;
+    c->chk_hi = ends_built && g_check ? g_hi : ni;
 
     // work-list sizes (exact: one record per F entry of a row genome)
     c->row_fprefix.assign(c->n_rows + 1, 0);
@@ -1188,8 +1362,12 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
     if (device_id < 0 || device_id >= ndev) return PFAAI_RC_INVALID;
     auto* c = new pfaai_ctx();
     c->device = device_id;
+    // the context stream at the highest priority: the load's side work (the
+    // both-given check's hash sums on copy_stream) fills what the sort leaves
+    int pri_least = 0, pri_greatest = 0;
     if (hipSetDevice(device_id) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipDeviceGetStreamPriorityRange(&pri_least, &pri_greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, pri_greatest) != hipSuccess) {
         delete c;
         return PFAAI_RC_HIP;
     }
@@ -1238,7 +1416,7 @@ int pfaai_destroy(pfaai_ctx* c) {
                       &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw, &c->srec_a, &c->srec_b, &c->shist,
-                      &c->sgsum, &c->sbase})
+                      &c->sgsum, &c->sbase, &c->tails, &c->ranks})
         release(*b);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->load_ev)
@@ -1265,6 +1443,12 @@ const char* pfaai_last_error(const pfaai_ctx* c) { return c ? c->err.c_str() : "
 int pfaai_load(pfaai_ctx* c, const pfaai_problem* pb) {
     if (!c || !pb) return PFAAI_RC_INVALID;
     return guarded(c, [&] { return load_impl(c, pb); });
+}
+
+int pfaai_load_rows(pfaai_ctx* c, const pfaai_problem* pb, int64_t row_begin, int64_t row_end) {
+    if (!c || !pb) return PFAAI_RC_INVALID;
+    if (row_begin < 0 || row_end < row_begin || row_end > pb->n_ids) return fail(c, PFAAI_RC_INVALID, "bad row range");
+    return guarded(c, [&] { return load_impl(c, pb, row_begin, row_end); });
 }
 
 int pfaai_shape(const pfaai_ctx* c, int64_t* n_rows, int64_t* n_pairs) {

@@ -62,10 +62,12 @@ __device__ __forceinline__ uint32_t sort_digit(uint64_t r, int shift, uint32_t m
 // F entry i -> key g * P + p (low 32 bits) | i << 32.  The histogram pass
 // also writes the u16 protein column of F that k_blk / k_blk_end read.
 struct SrcFKeys {
+    static constexpr bool kFilter = false;  // (SrcFEnds: records outside a genome range are dropped)  // (SrcFEnds: a per-tile pass over the records, see there)
     const int32_t* Fp;
     const int32_t* Fg;
     uint32_t P;
     uint16_t* fp16;  // nullable
+    __device__ __forceinline__ bool keep(uint64_t) const { return true; }
     __device__ __forceinline__ uint64_t hist_rec(int64_t i, bool valid) const {
         const int32_t p = Fp[i], g = Fg[i];
         if (fp16 && valid) fp16[i] = (uint16_t)p;
@@ -82,7 +84,9 @@ struct SrcFKeys {
 
 // materialised records (later passes; first passes of the keygen paths)
 struct SrcRecs {
+    static constexpr bool kFilter = false;
     const uint64_t* r;
+    __device__ __forceinline__ bool keep(uint64_t) const { return true; }
     __device__ __forceinline__ uint64_t hist_rec(int64_t i, bool) const { return r[i]; }
     __device__ __forceinline__ uint64_t load(int64_t i) const { return r[i]; }
     __device__ __forceinline__ uint64_t load_nt(int64_t i) const { return __builtin_nontemporal_load(r + i); }
@@ -99,7 +103,7 @@ struct DstRecs {
     static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t) const {
         r[pos] = v;
         return 0;
     }
@@ -120,11 +124,14 @@ struct DstRecs {
 // beyond their records (the first form checked list bounds by G_off[key],
 // G_off[key + 1] and read G_tet[pos] per record in the last pass: ~3 random
 // L2 requests per record, 3.4 ms of a 10k load's pass).
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser (a bijection)
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
+// xorshift-multiply-xorshift (a bijection of 64-bit words, nonlinear over
+// both Z_2^64 and GF(2)^64): one 64-bit multiply per lane -- the check runs
+// two lanes over every F and G entry beside the sort, and splitmix64's two
+// multiplies per lane made it the load's largest side cost (2.8 ms at 10k)
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 32;
+    x *= 0xD6E8FEB86659FD93ull;
+    return x ^ (x >> 32);
 }
 __device__ __forceinline__ uint64_t member_hash(uint64_t seed, uint32_t key, uint32_t t) {
     return mix64(seed ^ (((uint64_t)key << 18) | t));  // key < 2^32, t < 2^18 (host-checked): injective
@@ -136,7 +143,7 @@ struct DstGpos {
     static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t) const {
         G_pos[pos] = (uint32_t)(v >> 32);
         return 0;
     }
@@ -147,22 +154,27 @@ struct DstGpos {
 // per thread in flight, indices clamped rather than loads under a branch)
 // Two lanes (seed, seed2: independent per-load random keys; sums[0] and
 // sums[2]): a different multiset passes both with probability ~2^-128.
+// [g_lo, g_hi): only the entries of those genomes (a rank's rows, pfaai_load_rows).
 __global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                 const int32_t* __restrict__ Fg, uint32_t P, uint64_t seed,
-                                                uint64_t seed2, unsigned long long* __restrict__ sum) {
+                                                uint64_t seed2, unsigned long long* __restrict__ sum, int32_t g_lo,
+                                                int32_t g_hi) {
     uint64_t acc = 0, acc2 = 0;
     for (int t = blockIdx.x; t < kNTetramers; t += gridDim.x) {
         const int64_t b = Lp[t], e = Lp[t + 1];
         for (int64_t i0 = b + threadIdx.x; i0 < e; i0 += 4 * 256) {
             uint32_t key[4];
+            bool in[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int64_t i = min(i0 + u * 256, e - 1);
-                key[u] = (uint32_t)__builtin_nontemporal_load(Fg + i) * P + (uint32_t)__builtin_nontemporal_load(Fp + i);
+                const int32_t g = __builtin_nontemporal_load(Fg + i);
+                key[u] = (uint32_t)g * P + (uint32_t)__builtin_nontemporal_load(Fp + i);
+                in[u] = g >= g_lo && g < g_hi;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (i0 + u * 256 < e) {
+                if (i0 + u * 256 < e && in[u]) {
                     acc += member_hash(seed, key[u], (uint32_t)t);
                     acc2 += member_hash(seed2, key[u], (uint32_t)t);
                 }
@@ -201,7 +213,7 @@ struct DstGFromRecs {
         const int32_t t = (int32_t)((v >> kb) & 0x3FFFFu);
         return {(uint32_t)G_off[key], (uint32_t)G_off[key + 1], G_pos ? (uint32_t)Lp[t] : 0u};
     }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a) const {
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux a, int64_t) const {
         G_tet[pos] = (int32_t)((v >> kb) & 0x3FFFFu);
         if (G_pos) G_pos[pos] = a.lp + (uint32_t)(v >> (kb + 18));
         if (!(a.lo <= (uint64_t)pos && (uint64_t)pos < a.hi)) atomicOr(err, 1);
@@ -226,12 +238,378 @@ struct DstFFromG {
     static constexpr bool kSum = false;
     struct Aux {};
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
-    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux) const {
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t) const {
         const uint32_t p = (uint32_t)(v >> 18) & 0xFFFu, g = (uint32_t)(v >> 30) & 0x1FFFFFu;
         Fp[pos] = (int32_t)p;
         Fg[pos] = (int32_t)g;
         fp16[pos] = (uint16_t)p;
         Ft[pos] = (uint32_t)v & 0x3FFFFu;
+        return 0;
+    }
+};
+
+// ---- the F -> G sort that carries run ends (G_pos and G_end in one sort) ----
+// The all-vs-all row kernel walks, for every G entry (g, p, t), the F run
+// (t, p) from just past g (G_pos + 1) to the run's end (G_end).  G_pos is the
+// sorted position of F entry i in the F -> G sort (key g * P + p, F order is
+// t order); G_end is the end of i's run, known in F order.  So the first
+// pass's histogram kernel, which reads F tile by tile anyway, also finds the
+// runs of its tile (a run ends where the protein changes or a tetramer block
+// ends: a bitmap of block ends, k_block_ends) and writes each entry's
+// distance to its run end (D, u32; kOpenRun for the tile's last run when it
+// goes on into the next tiles -- its end is the first run end after the
+// tile, ntail, from k_tail_suffix); the first scatter carries the distance
+// in the record, the second writes G_pos and G_end side by side.  No run-end
+// table and no lookup per G entry (k_blk_end + k_gend: 2.1 ms of the 10k load).
+// Records: pass 1 key | rel << kb | dist << (kb + 12) | drop << 63 (rel: the
+// position in its 4096-entry tile), written as key >> db | i << hb | dist <<
+// (hb + 32) (hb = kb - db: the second digit, all that is left of the key);
+// a run spans < 2^21 entries (one per genome id).  drop: the genome lies
+// outside [g_lo, g_hi) (pfaai_load_rows: a rank builds the walk data of its
+// own rows only).
+
+constexpr uint32_t kNoTail = 0xFFFFFFFFu;
+constexpr uint32_t kOpenRun = 0xFFFFFFFFu;
+constexpr int kEndsTile = kSortNT * kSortItems;  // 4096 entries: the sort's tiles
+
+// bit i of bend: F position i is the last of a tetramer block
+__global__ void k_block_ends(const int64_t* __restrict__ Lp, uint32_t* __restrict__ bend) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x) {
+        const int64_t b = Lp[t], e = Lp[t + 1];
+        if (e > b) atomicOr(&bend[(e - 1) >> 5], 1u << ((uint32_t)(e - 1) & 31u));
+    }
+}
+
+// The both-given check's tetramer coordinate: the rank of a tetramer among
+// the NON-EMPTY blocks (rho), which the F side knows from the block-end
+// bitmap alone (rho(i) = block ends before position i) and the G side from
+// rho_t[t] (exclusive scan of the non-empty flags; a G tetramer whose F block
+// is empty maps to kNoRank and can never match).  Per tile: its block ends
+// (tcnt -> scan -> trank, the ends before the tile).
+__global__ void k_tile_ends(const uint32_t* __restrict__ bend, int64_t n, int64_t ntiles, uint32_t* __restrict__ tcnt) {
+    constexpr int W = kEndsTile / 32;
+    const int64_t nw = (n + 31) >> 5;
+    for (int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; T < ntiles; T += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t c = 0;
+        for (int w = 0; w < W; ++w) {
+            const int64_t x = T * W + w;
+            if (x < nw) c += __popc(bend[x]);
+        }
+        tcnt[T] = c;
+    }
+}
+__global__ void k_nonempty(const int64_t* __restrict__ Lp, uint32_t* __restrict__ flag) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x)
+        flag[t] = Lp[t + 1] > Lp[t] ? 1u : 0u;
+}
+constexpr uint32_t kNoRank = 0x3FFFFu;  // (18 bits: > every rank, < 2^18)
+// rank[t] = the rank of tetramer t among the non-empty blocks, kNoRank if empty
+__global__ void k_rank_table(const unsigned long long* __restrict__ rho, uint32_t* __restrict__ rank) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x)
+        rank[t] = rho[t + 1] > rho[t] ? (uint32_t)rho[t] : kNoRank;
+}
+
+// Pass 1's histogram over F (kept records only) + the u16 protein column +
+// each entry's distance to its run end (D) + the tile's first run end
+// (ftail, absolute).  Every global load is issued before the first store.
+template <int DB, int NT>
+__global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ Fp, const int32_t* __restrict__ Fg,
+                                                   const uint32_t* __restrict__ bend, int64_t n, uint32_t P,
+                                                   int32_t g_lo, int32_t g_hi, uint32_t mask,
+                                                   uint16_t* __restrict__ fp16, uint32_t* __restrict__ D,
+                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ ftail,
+                                                   uint32_t* __restrict__ ltail,
+                                                   const unsigned long long* __restrict__ trank, uint64_t seed,
+                                                   uint64_t seed2, unsigned long long* __restrict__ hpart) {
+    constexpr int BINS = 1 << DB, kTile = NT * kSortItems, kChunks = kTile / 64;
+    static_assert(kChunks <= 64, "one wave ballots the tile's chunks");
+    __shared__ uint32_t h[BINS];
+    __shared__ uint16_t sp[kTile + 1];              // protein of every position (+ the next tile's first)
+    __shared__ uint32_t sb[kTile / 32];             // block-end bits of the tile
+    __shared__ unsigned long long tm[kChunks];      // run-end bits
+    __shared__ uint8_t nextw[kChunks];              // next chunk holding a run end
+    __shared__ uint32_t first, last;
+    __shared__ uint32_t wpre[kTile / 32];          // block ends before each word of the tile (hpart)
+    __shared__ uint64_t hw[2 * (NT / 64)];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t tile = blockIdx.x, t0 = tile * kTile;
+    for (int b = tid; b < BINS; b += NT) h[b] = 0u;
+    int32_t p[kSortItems], g[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {
+        const int64_t i = min(t0 + (int64_t)(k * NT + tid), n - 1);
+        p[k] = __builtin_nontemporal_load(Fp + i);
+        g[k] = __builtin_nontemporal_load(Fg + i);
+    }
+    const int64_t nw = (n + 31) >> 5;
+    const uint32_t bw = tid < kTile / 32 ? bend[min(t0 / 32 + tid, nw - 1)] : 0u;
+    const int32_t p_next = t0 + kTile < n ? Fp[t0 + kTile] : -1;
+    __syncthreads();  // (h cleared)
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {
+        const int r = k * NT + tid;
+        const int64_t i = t0 + r;
+        sp[r] = (uint16_t)p[k];
+        if (i < n) {
+            if (fp16) fp16[i] = (uint16_t)p[k];
+            if (g[k] >= g_lo && g[k] < g_hi) atomicAdd(&h[((uint32_t)g[k] * P + (uint32_t)p[k]) & mask], 1u);
+        }
+    }
+    if (tid < kTile / 32) sb[tid] = bw;
+    if (tid == 0) sp[kTile] = (uint16_t)p_next;  // (-1: 0xFFFF, no protein id)
+    if (hpart && tid < kTile / 32) {  // exclusive prefix of the words' block ends (two waves)
+        const uint32_t pc = __popc(bw);
+        uint32_t inc = pc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        wpre[tid] = inc - pc;
+    }
+    __syncthreads();
+    if (hpart) {  // the F side of the both-given check: h(g * P + p, rho) over the kept entries
+        const uint32_t carry = wpre[63] + __popc(sb[63]);  // (ends in the tile's first 64 words)
+        const unsigned long long rb = trank[tile];
+        uint64_t acc = 0, acc2 = 0;
+#pragma unroll
+        for (int k = 0; k < kSortItems; ++k) {
+            const int r = k * NT + tid;
+            const int64_t i = t0 + r;
+            const uint32_t w = (uint32_t)r >> 5;
+            const uint32_t rho = (uint32_t)rb + wpre[w] + (w >= 64 ? carry : 0u) + __popc(sb[w] & ((1u << (r & 31)) - 1u));
+            if (i < n && g[k] >= g_lo && g[k] < g_hi) {
+                const uint32_t key = (uint32_t)g[k] * P + (uint32_t)p[k];
+                acc += member_hash(seed, key, rho);
+                acc2 += member_hash(seed2, key, rho);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc += __shfl_down(acc, o, 64);
+            acc2 += __shfl_down(acc2, o, 64);
+        }
+        // the tile's sums to hpart[tile] (k_tail_suffix adds them up: one
+        // atomic per wave into one address serialised at ~10 ns each)
+        if (lane == 0) {
+            hw[2 * (tid >> 6)] = acc;
+            hw[2 * (tid >> 6) + 1] = acc2;
+        }
+        __syncthreads();
+        if (tid < 2) {
+            uint64_t x = 0;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) x += hw[2 * w + tid];
+            hpart[2 * tile + tid] = x;
+        }
+    }
+#pragma unroll 1
+    for (int k = 0; k < kSortItems; ++k) {  // run ends, one 64-position chunk per (wave, k) ballot
+        const int r = k * NT + tid;
+        const int64_t i = t0 + r;
+        const bool tail = i < n && (i == n - 1 || ((sb[r >> 5] >> (r & 31)) & 1u) || sp[r] != sp[r + 1]);
+        const unsigned long long m = __ballot(tail);
+        if (lane == 0) tm[r >> 6] = m;
+    }
+    __syncthreads();
+    if (tid < kChunks) {
+        const unsigned long long b =
+            __ballot(tm[tid] != 0ull) & (kChunks == 64 ? ~0ull : ((1ull << kChunks) - 1ull));
+        const unsigned long long after = tid == 63 ? 0ull : b >> (tid + 1);
+        nextw[tid] = after ? (uint8_t)(tid + 1 + __builtin_ctzll(after)) : (uint8_t)kChunks;
+        if (tid == 0) first = b ? (uint32_t)(__builtin_ctzll(b) * 64 + __builtin_ctzll(tm[__builtin_ctzll(b)])) : kNoTail;
+        if (tid == 0) {
+            const int wl = b ? 63 - __builtin_clzll(b) : 0;
+            last = b ? (uint32_t)(wl * 64 + 63 - __builtin_clzll(tm[wl])) : kNoTail;
+        }
+    }
+    __syncthreads();
+    for (int b = tid; b < BINS; b += NT) hist[tile * BINS + b] = h[b];
+    if (tid == 0) {
+        ftail[tile] = first == kNoTail ? kNoTail : (uint32_t)(t0 + first);
+        ltail[tile] = last;  // (tile-relative: the tile's open run starts after it)
+    }
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {
+        const uint32_t r = (uint32_t)(k * NT + tid);
+        const uint32_t w = r >> 6;
+        const unsigned long long m = tm[w] & (~0ull << (r & 63u));
+        uint32_t d = kOpenRun;
+        if (m) {
+            d = (w << 6) + (uint32_t)__builtin_ctzll(m) + 1u - r;
+        } else {
+            const uint32_t w2 = nextw[w];
+            if (w2 < (uint32_t)kChunks) d = (w2 << 6) + (uint32_t)__builtin_ctzll(tm[w2]) + 1u - r;
+        }
+        if (t0 + r < n) D[t0 + r] = d;
+    }
+}
+
+// ntail[T] = the smallest ftail over tiles T' > T (one workgroup; position
+// n - 1 ends a run, so every tile but the last has one after it)
+__global__ __launch_bounds__(1024) void k_tail_suffix(const uint32_t* __restrict__ ftail, int64_t ntiles,
+                                                     uint32_t* __restrict__ ntail) {
+    __shared__ uint32_t cm[1024];
+    const int tid = threadIdx.x;
+    const int64_t C = (ntiles + 1023) / 1024, lo = tid * C, hi = min(ntiles, lo + C);
+    uint32_t m = kNoTail;
+    for (int64_t T = lo; T < hi; ++T) m = min(m, ftail[T]);
+    cm[tid] = m;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive suffix minimum over threads
+        const uint32_t v = tid + o < 1024 ? cm[tid + o] : kNoTail;
+        __syncthreads();
+        cm[tid] = min(cm[tid], v);
+        __syncthreads();
+    }
+    uint32_t run = tid + 1 < 1024 ? cm[tid + 1] : kNoTail;
+    for (int64_t T = hi - 1; T >= lo; --T) {
+        ntail[T] = run;
+        run = min(run, ftail[T]);
+    }
+}
+
+// The open runs' distances: in tile T the entries after its last run end
+// (ltail) belong to a run that ends at the first run end after the tile
+// (ntail[T]).  One wave per tile.
+__global__ __launch_bounds__(256) void k_fix_open(const uint32_t* __restrict__ ltail, const uint32_t* __restrict__ ntail,
+                                                  int64_t ntiles, int64_t n, uint32_t* __restrict__ D) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t T = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; T < ntiles;
+         T += (int64_t)gridDim.x * blockDim.x / 64) {
+        const int64_t t0 = T * kEndsTile;
+        const uint32_t lt = ltail[T];
+        const int64_t b = t0 + (lt == kNoTail ? 0 : (int64_t)lt + 1), e = min(n, t0 + kEndsTile);
+        const int64_t end = (int64_t)ntail[T] + 1;
+        for (int64_t i = b + lane; i < e; i += 64) D[i] = (uint32_t)(end - i);
+    }
+}
+
+// sum[0] += sum of part[2 k], sum[2] += sum of part[2 k + 1] (the check's
+// per-tile F sums; one atomic pair per workgroup)
+__global__ __launch_bounds__(256) void k_sum_pairs(const unsigned long long* __restrict__ part, int64_t n,
+                                                   unsigned long long* __restrict__ sum) {
+    __shared__ uint64_t ws[2 * 4];
+    uint64_t a = 0, b = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        a += part[2 * k];
+        b += part[2 * k + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_down(a, o, 64);
+        b += __shfl_down(b, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ws[2 * (threadIdx.x >> 6)] = a;
+        ws[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(sum, (unsigned long long)(ws[0] + ws[2] + ws[4] + ws[6]));
+        atomicAdd(sum + 2, (unsigned long long)(ws[1] + ws[3] + ws[5] + ws[7]));
+    }
+}
+
+// The G side of the run-end sort's check: sum over the lists (g, p), g in
+// [g_lo, g_hi), of h(g * P + p, rank[G_tet]) in two lanes -- one wave per
+// list (no search for an entry's list), four entries per lane in flight;
+// one atomic pair per workgroup.
+__global__ __launch_bounds__(256) void k_hash_g(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
+                                                int32_t P, int32_t g_lo, int32_t g_hi,
+                                                const uint32_t* __restrict__ rank, uint64_t seed, uint64_t seed2,
+                                                unsigned long long* __restrict__ sum) {
+    __shared__ uint64_t ws[2 * 4];
+    const int lane = threadIdx.x & 63;
+    const int64_t l_lo = (int64_t)g_lo * P, l_hi = (int64_t)g_hi * P;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    uint64_t a = 0, b = 0;
+    for (int64_t l = l_lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); l < l_hi; l += waves) {
+        const int64_t e0 = G_off[l], e1 = G_off[l + 1];
+        const uint32_t key = (uint32_t)l;  // = g * P + p
+        for (int64_t k0 = e0 + lane; k0 < e1; k0 += 4 * 64) {
+            uint32_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t[u] = (uint32_t)__builtin_nontemporal_load(G_tet + min(k0 + u * 64, e1 - 1));
+            uint32_t r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = rank[t[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k0 + u * 64 < e1) {
+                    a += member_hash(seed, key, r[u]);
+                    b += member_hash(seed2, key, r[u]);
+                }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_down(a, o, 64);
+        b += __shfl_down(b, o, 64);
+    }
+    if (lane == 0) {
+        ws[2 * (threadIdx.x >> 6)] = a;
+        ws[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(sum, (unsigned long long)(ws[0] + ws[2] + ws[4] + ws[6]));
+        atomicAdd(sum + 2, (unsigned long long)(ws[1] + ws[3] + ws[5] + ws[7]));
+    }
+}
+
+// F entry i -> pass 1's record, its distance to its run end from D
+struct SrcFEnds {
+    static constexpr bool kFilter = true;
+    const int32_t* Fp;
+    const int32_t* Fg;
+    const uint32_t* D;
+    uint32_t P;
+    int kb;
+    int32_t g_lo, g_hi;
+    __device__ __forceinline__ bool keep(uint64_t r) const { return !(r >> 63); }
+    __device__ __forceinline__ uint64_t rec(int64_t i, int32_t g, int32_t p, uint32_t d) const {
+        return (uint64_t)((uint32_t)g * P + (uint32_t)p) | ((uint64_t)(i & (kEndsTile - 1)) << kb) |
+               ((uint64_t)(d & 0x1FFFFFu) << (kb + 12)) | ((uint64_t)(g < g_lo || g >= g_hi) << 63);
+    }
+    __device__ __forceinline__ uint64_t load(int64_t i) const { return rec(i, Fg[i], Fp[i], D[i]); }
+    __device__ __forceinline__ uint64_t load_nt(int64_t i) const {
+        return rec(i, __builtin_nontemporal_load(Fg + i), __builtin_nontemporal_load(Fp + i),
+                   __builtin_nontemporal_load(D + i));
+    }
+};
+
+// pass 1's records out: the second digit, the F index, the distance to its run end
+struct DstRecsEnds {
+    uint64_t* r;
+    int kb, db;
+    static constexpr int kWH = kSortItems;
+    static constexpr bool kSum = false;
+    struct Aux {};
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t t0) const {
+        const int hb = kb - db;
+        const uint64_t key = v & ((1ull << kb) - 1ull);
+        const uint64_t i = (uint64_t)t0 + ((v >> kb) & 0xFFFull);
+        const uint64_t dist = (v >> (kb + 12)) & 0x1FFFFFull;
+        r[pos] = (key >> db) | (i << hb) | (dist << (hb + 32));
+        return 0;
+    }
+};
+
+// pass 2 (G order): G_pos = the F index, G_end = its run end
+struct DstGposEnds {
+    uint32_t* G_pos;
+    uint32_t* G_end;
+    int hb;
+    static constexpr int kWH = kSortItems;
+    static constexpr bool kSum = false;
+    struct Aux {};
+    __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
+    __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t) const {
+        const uint32_t i = (uint32_t)(v >> hb), dist = (uint32_t)(v >> (hb + 32));
+        G_pos[pos] = i;
+        G_end[pos] = i + dist;
         return 0;
     }
 };
@@ -451,6 +829,7 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
     };
     int64_t tile = dyn ? next_tile(0) : tile0;
     fetch_tile(tile < tend ? tile : ntiles, rec, gb);
+    __shared__ uint32_t s_tn;  // records of the tile that pass Src::keep
     while (tile < tend) {
         const int64_t t0 = tile * kTile;
         int64_t tnext = 0;
@@ -471,7 +850,7 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
         uint16_t lr[kSortItems];
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
-            const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n;
+            const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n && src.keep(rec[k]);
             const uint32_t d = sort_digit(rec[k], shift, mask);
             uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -532,6 +911,7 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             if (b < BINS) lstart[b] = off;
             off += tot[q];
         }
+        if (tid == NT - 1) s_tn = off;  // (the tile's records, all digits)
         __syncthreads();
         {
             uint32_t slot[kSortItems];  // every LDS read issued before the first write
@@ -542,12 +922,12 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             }
 #pragma unroll
             for (int k = 0; k < kSortItems; ++k)
-                if (t0 + (wid * kSortItems + k) * 64 + lane < n) srt[slot[k]] = rec[k];
+                if (t0 + (wid * kSortItems + k) * 64 + lane < n && src.keep(rec[k])) srt[slot[k]] = rec[k];
         }
         __syncthreads();
         // write the tile in digit order: each digit's run is contiguous in the output
         // (positions are < 2^32: n <= 2^32 - 64; records re-read from LDS for the stores)
-        const int tn = (int)((n - t0) < kTile ? (n - t0) : kTile);
+        const int tn = Src::kFilter ? (int)s_tn : (int)((n - t0) < kTile ? (n - t0) : kTile);
         // (unconditional reads at positions clamped into the tile: no wait per item)
 #pragma unroll
         for (int h = 0; h < kSortItems; h += kWH) {  // kWH records per thread in flight
@@ -556,12 +936,12 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             typename Dst::Aux aux[kWH];
 #pragma unroll
             for (int k = 0; k < kWH; ++k) {
-                const int lp = min(tid + (h + k) * NT, tn - 1);
+                const int lp = min(tid + (h + k) * NT, max(tn - 1, 0));
                 val[k] = srt[lp];
             }
 #pragma unroll
             for (int k = 0; k < kWH; ++k) {
-                const int lp = min(tid + (h + k) * NT, tn - 1);
+                const int lp = min(tid + (h + k) * NT, max(tn - 1, 0));
                 const uint32_t d = sort_digit(val[k], shift, mask);
                 pos[k] = gbase[d] + (uint32_t)(lp - (int)lstart[d]);
             }
@@ -570,7 +950,7 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
 #pragma unroll
             for (int k = 0; k < kWH; ++k) {
                 const int lp = tid + (h + k) * NT;
-                if ((VAR & 8) == 0 && lp < tn) hsum += dst.store(pos[k], val[k], aux[k]);
+                if ((VAR & 8) == 0 && lp < tn) hsum += dst.store(pos[k], val[k], aux[k], t0);
             }
         }
         __syncthreads();  // the LDS tile, counters and bases are rewritten by the next tile
@@ -676,7 +1056,8 @@ __global__ void k_len_from_t(const int32_t* __restrict__ T, int32_t P, int32_t n
 //         per load, so the WK 3 row kernel reads (G_pos, G_end) coalesced;
 //   HASH: the G side of the both-given check (DstGpos): sums[0] +=
 //         h(list of k, G_tet[k]) and, keyed by seed2, sums[2] (k_hash_f's
-//         second lane).
+//         second lane); with rho, h(list of k, rank of G_tet[k] among the
+//         non-empty F blocks) -- the F side then comes from k_fends_hist.
 // The lists are taken protein-major (all genomes of protein p, then p + 1),
 // so the table lookups in flight hit one or two protein rows (640 KB each),
 // which stay in every XCD's L2 -- genome-major order touched all 100 rows at
@@ -690,7 +1071,8 @@ template <bool END, bool HASH>
 __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
                                               int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
                                               uint32_t* __restrict__ G_end, uint64_t seed, uint64_t seed2,
-                                              unsigned long long* __restrict__ sums) {
+                                              unsigned long long* __restrict__ sums, int32_t g_lo,
+                                              int32_t g_hi, const uint32_t* __restrict__ rank) {
     __shared__ int64_t lb[kGendLists];
     __shared__ uint32_t pre[kGendLists + 1];
     __shared__ int64_t row[kGendLists];
@@ -703,12 +1085,12 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
             uint32_t len = 0;
             if (tid < kGendLists) {
                 const int64_t q = min(q0 + tid, n_lists - 1);
-                const int64_t p = q / n_ids, L = (q - p * n_ids) * P + p;
+                const int64_t p = q / n_ids, g = q - p * n_ids, L = g * P + p;
                 const int64_t b = G_off[L], e = G_off[L + 1];
                 lb[tid] = b;
                 row[tid] = p * kNTetramers;
                 lid[tid] = (uint32_t)L;
-                len = q0 + tid < n_lists ? (uint32_t)(e - b) : 0u;
+                len = q0 + tid < n_lists && g >= g_lo && g < g_hi ? (uint32_t)(e - b) : 0u;
             }
             uint32_t inc = len;
 #pragma unroll
@@ -750,8 +1132,11 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
                 if (f0 + (uint32_t)u * 256u < total) {
                     if constexpr (END) G_end[k[u]] = v[u];
                     if constexpr (HASH) {
-                        hm += member_hash(seed, li[u], (uint32_t)t[u]);
-                        hm2 += member_hash(seed2, li[u], (uint32_t)t[u]);
+                        // rho (the run-end sort's check): the rank of t among the non-empty F blocks
+                        uint32_t x = (uint32_t)t[u];
+                        if (rank) x = rank[x];
+                        hm += member_hash(seed, li[u], x);
+                        hm2 += member_hash(seed2, li[u], x);
                     }
                 }
             }

@@ -63,6 +63,18 @@ def split_range(row_lo: int, row_hi: int, parts: int, n_rows: int, all_vs_all: b
     return [(cuts[i], cuts[i + 1]) for i in range(parts)]
 
 
+def row_costs(n_rows: int, all_vs_all: bool = True, fixed_cols: float | None = None):
+    """The model cost of every output row (numpy float64[n_rows]): fixed +
+    width for all-vs-all row a (width n-1-a), 1 per row otherwise -- the
+    density split_rows cuts into equal shares."""
+    import numpy as np
+
+    if not all_vs_all:
+        return np.ones(n_rows)
+    k = FIXED_COST_FRACTION * n_rows if fixed_cols is None else float(fixed_cols)
+    return k + (n_rows - 1 - np.arange(n_rows, dtype=np.float64))
+
+
 class PipelinedGather:
     """Row blocks cut into `chunks` pipeline chunks per rank.  Chunk j of every
     rank has its own buffer (padded to the largest rank's chunk j); issue(j)

@@ -6,6 +6,8 @@ g (G only: F built).  The library comes from PFAAI_HIP_LIB (the diagnostics
 build reads the A/B switch PFAAI_TSORT_DB, the sort's digit width).
 
     python tools/gpu/load_bench.py --genomes 10000 --orient both --reps 3
+    python tools/gpu/load_bench.py --parts 8      # each rank's load of an 8-way
+                                                  # row split (pfaai_load_rows)
 """
 import argparse
 import json
@@ -23,6 +25,7 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--orient", choices=["both", "f", "g"], default="both")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--parts", type=int, default=1, help="per-rank loads of a K-way row split (pfaai_load_rows)")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime per process)
     from parfastaai_amd import _capi, syn
@@ -37,13 +40,17 @@ def main():
     print(f"[load_bench] SYN {a.genomes} x {a.prot} |F| = {len(g['F_genome'])} in {time.perf_counter() - t0:.1f}s",
           file=sys.stderr, flush=True)
     eng = _capi.Engine(0, lib_path=os.environ.get("PFAAI_HIP_LIB"))
-    dev = []
-    for _ in range(a.reps):
-        eng.load(**pb)
-        dev.append(round(eng.load_timing()[2], 3))
-    print(json.dumps({"genomes": a.genomes, "prot": a.prot, "F": len(g["F_genome"]), "orient": a.orient,
-                      "path": eng.load_info(), "device_ms": dev, "tsort_db": os.environ.get("PFAAI_TSORT_DB")}),
-          flush=True)
+    from parfastaai_amd.shard import split_rows
+
+    blocks = [None] if a.parts <= 1 else split_rows(a.genomes, a.parts)
+    for blk in blocks:
+        dev = []
+        for _ in range(a.reps):
+            eng.load(**pb, rows=blk)
+            dev.append(round(eng.load_timing()[2], 3))
+        print(json.dumps({"genomes": a.genomes, "prot": a.prot, "F": len(g["F_genome"]), "orient": a.orient,
+                          "rows": list(blk) if blk else "all", "path": eng.load_info(), "device_ms": dev,
+                          "tsort_db": os.environ.get("PFAAI_TSORT_DB")}), flush=True)
     eng.close()
 
 
