@@ -355,7 +355,8 @@ def main():
     # a rank loads the whole input but builds the walk data (G_pos / G_end,
     # the run-end sort) of its own row block only (pfaai_load_rows); all-vs-all
     # rows are genomes, so the blocks are known before the load
-    blocks = split_rows(args.genomes, world)
+    # (cus: cuts a few rows past a round of 2 x CUs row workgroups move back)
+    blocks = split_rows(args.genomes, world, cus=torch.cuda.get_device_properties(dev).multi_processor_count)
     t0 = time.perf_counter()
     eng.load(**ds.problem(), rows=blocks[rank] if world > 1 else None)
     load_wall_ms = (time.perf_counter() - t0) * 1e3

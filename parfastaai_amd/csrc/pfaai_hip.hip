@@ -680,8 +680,9 @@ int build_gpos_from_f(pfaai_ctx* c, int64_t n_f, hipStream_t s) {
 // (pfaai_sort.hpp: k_block_ends, k_fends_hist writes each entry's distance to
 // its run end, SrcFEnds / DstRecsEnds / DstGposEnds): two passes over F and no
 // run-end table or per-entry lookup.  check (seeds): the both-given
-// membership sums of those genomes (F side k_hash_f, G side k_gend HASH) run
-// on the second stream beside the scatters.  Returns -1 where the records do
+// membership sums of those genomes -- the F side in k_fends_hist (per tile,
+// added up by k_sum_pairs), the G side (k_hash_g) on the second stream
+// beside the whole sort.  Returns -1 where the records do
 // not fit two passes (the caller takes check_g_transpose / the plain G_pos
 // sort + k_blk_end + k_gend).
 template <int DB>
@@ -698,11 +699,11 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
     uint32_t* tctr = base + (1 << DB);
     auto* bend = static_cast<uint32_t*>(c->tails.p);
     const int64_t nwords = ceil_div(n_f, 32);
-    uint32_t* ftail = bend + nwords;
+    uint32_t* tcnt = bend + nwords;    // block ends per tile (the check's ranks; zeroed with bend)
+    uint32_t* ftail = tcnt + ntiles;
     uint32_t* ntail = ftail + ntiles;
     uint32_t* ltail = ntail + ntiles;
-    uint32_t* tcnt = ltail + ntiles;   // block ends per tile (the check's ranks)
-    uint32_t* flag = tcnt + ntiles;    // non-empty tetramer blocks, then their ranks (k_gend's lookups)
+    uint32_t* flag = ltail + ntiles;   // non-empty tetramer blocks, then the list of them (tnz)
     auto* trank = static_cast<unsigned long long*>(c->ranks.p);  // [ntiles + 1]
     unsigned long long* rho = trank + ntiles + 1;                // [160001]
     unsigned long long* hpart = rho + kNTetramers + 1;           // [2 * ntiles]: the F side's per-tile sums
@@ -711,37 +712,37 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
     const auto* Lp = static_cast<const int64_t*>(c->Lp.p);
     const auto* Fp = static_cast<const int32_t*>(c->Fp.p);
     const auto* Fg = static_cast<const int32_t*>(c->Fg.p);
-    HIPCHK(c, hipMemsetAsync(bend, 0, nwords * 4, s));
-    if (seeds) HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_block_ends, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, Lp, bend);
-    if (seeds) {  // the check's tetramer ranks (pfaai_sort.hpp k_tile_ends / k_nonempty)
-        hipLaunchKernelGGL(k_tile_ends, dim3((int)std::min<int64_t>(ceil_div(ntiles, 256), 4096)), dim3(256), 0, s, bend,
-                           n_f, ntiles, tcnt);
-        hipLaunchKernelGGL(k_nonempty, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, Lp, flag);
+    HIPCHK(c, hipMemsetAsync(bend, 0, (nwords + (seeds ? ntiles : 0)) * 4, s));
+    if (seeds) {  // the G side of the check (reads G only) beside the whole sort: 0.34 ms alone at 10k
+        HIPCHK(c, hipMemsetAsync(sc + SC_HF, 0, 4 * sizeof(unsigned long long), s));
+        HIPCHK(c, hipEventRecord(c->side_ev[0], s));
+        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->side_ev[0], 0));
+        const int64_t nch = ceil_div((int64_t)(g_hi - g_lo) * P, 64);
+        hipLaunchKernelGGL(k_hash_g, dim3((int)std::clamp<int64_t>(ceil_div(nch, 4), 1, 2048)), dim3(256), 0,
+                           c->copy_stream, static_cast<const int64_t*>(c->G_off.p),
+                           static_cast<const int32_t*>(c->G_tet.p), P, g_lo, g_hi, seeds[0], seeds[1], sc + SC_HG);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->side_ev[1], c->copy_stream));
+    }
+    hipLaunchKernelGGL(k_block_ends, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, Lp, bend,
+                       seeds ? tcnt : nullptr, flag);
+    if (seeds) {  // the F side's tetramers: block ranks per tile, the non-empty blocks (k_tnz)
         int rc;
         if ((rc = scan_u32(c, tcnt, ntiles, trank, s)) || (rc = scan_u32(c, flag, kNTetramers, rho, s))) return rc;
-        hipLaunchKernelGGL(k_rank_table, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, rho, flag);
+        hipLaunchKernelGGL(k_tnz, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, rho, flag);
     }
     const uint32_t mask1 = (1u << DB) - 1u, mask2 = (1u << hb) - 1u;
     hipLaunchKernelGGL((k_fends_hist<DB, NT>), dim3(ntiles), dim3(NT), 0, s, Fp, Fg, bend, n_f, (uint32_t)P, g_lo, g_hi,
-                       mask1, static_cast<uint16_t*>(c->Fp16.p), D, hist, ftail, ltail, trank,
+                       mask1, static_cast<uint16_t*>(c->Fp16.p), D, hist, ftail, ltail, trank, flag,
                        seeds ? seeds[0] : 0ull, seeds ? seeds[1] : 0ull, seeds ? hpart : nullptr);
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(k_tail_suffix, dim3(1), dim3(1024), 0, s, ftail, ntiles, ntail);
+    hipLaunchKernelGGL(k_tail_suffix, dim3((int)std::min<int64_t>(ceil_div(ntiles, 256), 4096)), dim3(256), 0, s, ftail,
+                       ntiles, ntail);
     hipLaunchKernelGGL(k_fix_open, dim3((int)std::min<int64_t>(ceil_div(ntiles, 4), 65536)), dim3(256), 0, s, ltail, ntail,
                        ntiles, n_f, D);
     hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ngroups), dim3(kSortThreads), 0, s, hist, ntiles, gsum);
     hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ngroups, base, tctr);
-    if (seeds) {  // the sums of the check beside the scatters: the F side's tiles, the G side
-        HIPCHK(c, hipEventRecord(c->side_ev[0], s));
-        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->side_ev[0], 0));
-        hipLaunchKernelGGL(k_sum_pairs, dim3(256), dim3(256), 0, c->copy_stream, hpart, ntiles, sc + SC_HF);
-        hipLaunchKernelGGL(k_hash_g, dim3(2048), dim3(256), 0, c->copy_stream, static_cast<const int64_t*>(c->G_off.p),
-                           static_cast<const int32_t*>(c->G_tet.p), P, g_lo, g_hi, flag, seeds[0], seeds[1],
-                           sc + SC_HG);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipEventRecord(c->side_ev[1], c->copy_stream));
-    }
+    if (seeds) hipLaunchKernelGGL(k_sum_pairs, dim3(256), dim3(256), 0, s, hpart, ntiles, sc + SC_HF);
     const size_t lds = sort_scatter_lds<DB, NT>();
     int cus = 256, per1 = 1, per2 = 1;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -750,7 +751,7 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per2, reinterpret_cast<const void*>(&k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>), NT, lds);
     auto* rec = static_cast<uint64_t*>(c->srec_a.p);
-    const SrcFEnds src{Fp, Fg, D, (uint32_t)P, kb, g_lo, g_hi};
+    const SrcFEnds src{Fp, Fg, D, (uint32_t)P, kb, g_lo, g_hi, 2 * n_kept < n_f};
     hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcFEnds, DstRecsEnds>),
                        dim3((int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per1))), dim3(NT), lds, s, src,
                        DstRecsEnds{rec, kb, DB}, n_f, ntiles, 0, mask1, hist, gsum, base, tctr);
@@ -1299,17 +1300,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
             auto* gend = static_cast<uint32_t*>(c->G_end.p);
             if (g_check)
                 hipLaunchKernelGGL((k_gend<true, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, check_seed, check_seed2, sums, 0, ni, nullptr);
+                                   gend, check_seed, check_seed2, sums, 0, ni);
             else
                 hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
-                                   gend, 0ull, 0ull, nullptr, 0, ni, nullptr);
+                                   gend, 0ull, 0ull, nullptr, 0, ni);
             HIPCHK(c, hipGetLastError());
             d.G_end = static_cast<const uint32_t*>(c->G_end.p);
         } else {
             release(c->G_end);
             if (g_check) {
                 hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
-                                   nullptr, nullptr, check_seed, check_seed2, sums, 0, ni, nullptr);
+                                   nullptr, nullptr, check_seed, check_seed2, sums, 0, ni);
                 HIPCHK(c, hipGetLastError());
             }
         }

@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t sort_digit(uint64_t r, int shift, uint32_t m
 // F entry i -> key g * P + p (low 32 bits) | i << 32.  The histogram pass
 // also writes the u16 protein column of F that k_blk / k_blk_end read.
 struct SrcFKeys {
-    static constexpr bool kFilter = false;  // (SrcFEnds: records outside a genome range are dropped)  // (SrcFEnds: a per-tile pass over the records, see there)
+    static constexpr bool kFilter = false;  // (SrcFEnds: records outside a genome range are dropped)
     const int32_t* Fp;
     const int32_t* Fg;
     uint32_t P;
@@ -272,41 +272,32 @@ constexpr uint32_t kNoTail = 0xFFFFFFFFu;
 constexpr uint32_t kOpenRun = 0xFFFFFFFFu;
 constexpr int kEndsTile = kSortNT * kSortItems;  // 4096 entries: the sort's tiles
 
-// bit i of bend: F position i is the last of a tetramer block
-__global__ void k_block_ends(const int64_t* __restrict__ Lp, uint32_t* __restrict__ bend) {
+// bit i of bend: F position i is the last of a tetramer block; with tcnt
+// (the check) also the block ends per tile (tcnt, zeroed) and the non-empty
+// flags of the blocks (flag)
+__global__ void k_block_ends(const int64_t* __restrict__ Lp, uint32_t* __restrict__ bend, uint32_t* __restrict__ tcnt,
+                             uint32_t* __restrict__ flag) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x) {
         const int64_t b = Lp[t], e = Lp[t + 1];
         if (e > b) atomicOr(&bend[(e - 1) >> 5], 1u << ((uint32_t)(e - 1) & 31u));
+        if (tcnt) {
+            flag[t] = e > b ? 1u : 0u;
+            if (e > b) atomicAdd(&tcnt[(e - 1) / kEndsTile], 1u);
+        }
     }
 }
 
-// The both-given check's tetramer coordinate: the rank of a tetramer among
-// the NON-EMPTY blocks (rho), which the F side knows from the block-end
-// bitmap alone (rho(i) = block ends before position i) and the G side from
-// rho_t[t] (exclusive scan of the non-empty flags; a G tetramer whose F block
-// is empty maps to kNoRank and can never match).  Per tile: its block ends
-// (tcnt -> scan -> trank, the ends before the tile).
-__global__ void k_tile_ends(const uint32_t* __restrict__ bend, int64_t n, int64_t ntiles, uint32_t* __restrict__ tcnt) {
-    constexpr int W = kEndsTile / 32;
-    const int64_t nw = (n + 31) >> 5;
-    for (int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; T < ntiles; T += (int64_t)gridDim.x * blockDim.x) {
-        uint32_t c = 0;
-        for (int w = 0; w < W; ++w) {
-            const int64_t x = T * W + w;
-            if (x < nw) c += __popc(bend[x]);
-        }
-        tcnt[T] = c;
-    }
-}
-__global__ void k_nonempty(const int64_t* __restrict__ Lp, uint32_t* __restrict__ flag) {
+// The both-given check's tetramer: the F side knows the rank of an entry's
+// block among the NON-EMPTY blocks from the block-end bitmap alone (rho(i) =
+// block ends before position i; per tile: its block ends, tcnt -> scan ->
+// trank; k_block_ends counts them) and takes the tetramer from the list of non-empty blocks (tnz[rho],
+// one table row per run of equal rho: the wave's loads coalesce); the G side
+// hashes G_tet as it is, so it needs nothing from F and runs from the start
+// of the load (k_hash_g).
+// tnz[r] = the r-th non-empty tetramer (rho: exclusive scan of the flags)
+__global__ void k_tnz(const unsigned long long* __restrict__ rho, uint32_t* __restrict__ tnz) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x)
-        flag[t] = Lp[t + 1] > Lp[t] ? 1u : 0u;
-}
-constexpr uint32_t kNoRank = 0x3FFFFu;  // (18 bits: > every rank, < 2^18)
-// rank[t] = the rank of tetramer t among the non-empty blocks, kNoRank if empty
-__global__ void k_rank_table(const unsigned long long* __restrict__ rho, uint32_t* __restrict__ rank) {
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < kNTetramers; t += gridDim.x * blockDim.x)
-        rank[t] = rho[t + 1] > rho[t] ? (uint32_t)rho[t] : kNoRank;
+        if (rho[t + 1] > rho[t]) tnz[rho[t]] = (uint32_t)t;
 }
 
 // Pass 1's histogram over F (kept records only) + the u16 protein column +
@@ -319,7 +310,8 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
                                                    uint16_t* __restrict__ fp16, uint32_t* __restrict__ D,
                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ ftail,
                                                    uint32_t* __restrict__ ltail,
-                                                   const unsigned long long* __restrict__ trank, uint64_t seed,
+                                                   const unsigned long long* __restrict__ trank,
+                                                   const uint32_t* __restrict__ tnz, uint64_t seed,
                                                    uint64_t seed2, unsigned long long* __restrict__ hpart) {
     constexpr int BINS = 1 << DB, kTile = NT * kSortItems, kChunks = kTile / 64;
     static_assert(kChunks <= 64, "one wave ballots the tile's chunks");
@@ -331,8 +323,14 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
     __shared__ uint32_t first, last;
     __shared__ uint32_t wpre[kTile / 32];          // block ends before each word of the tile (hpart)
     __shared__ uint64_t hw[2 * (NT / 64)];
+    __shared__ uint32_t stz[64];                   // the tile's first 64 tetramers (hpart)
     const int tid = threadIdx.x, lane = tid & 63;
     const int64_t tile = blockIdx.x, t0 = tile * kTile;
+    const unsigned long long rb = hpart ? trank[tile] : 0ull;
+    if (hpart && tid < 64) {
+        const unsigned long long ix = rb + (unsigned long long)tid;
+        stz[tid] = tnz[ix < (unsigned long long)kNTetramers ? (int64_t)ix : (int64_t)kNTetramers - 1];
+    }
     for (int b = tid; b < BINS; b += NT) h[b] = 0u;
     int32_t p[kSortItems], g[kSortItems];
 #pragma unroll
@@ -368,9 +366,8 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
         wpre[tid] = inc - pc;
     }
     __syncthreads();
-    if (hpart) {  // the F side of the both-given check: h(g * P + p, rho) over the kept entries
+    if (hpart) {  // the F side of the both-given check: h(g * P + p, t) over the kept entries
         const uint32_t carry = wpre[63] + __popc(sb[63]);  // (ends in the tile's first 64 words)
-        const unsigned long long rb = trank[tile];
         uint64_t acc = 0, acc2 = 0;
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
@@ -378,10 +375,12 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
             const int64_t i = t0 + r;
             const uint32_t w = (uint32_t)r >> 5;
             const uint32_t rho = (uint32_t)rb + wpre[w] + (w >= 64 ? carry : 0u) + __popc(sb[w] & ((1u << (r & 31)) - 1u));
+            const uint32_t rl = rho - (uint32_t)rb;
+            const uint32_t t = rl < 64u ? stz[rl] : tnz[i < n ? rho : 0u];
             if (i < n && g[k] >= g_lo && g[k] < g_hi) {
                 const uint32_t key = (uint32_t)g[k] * P + (uint32_t)p[k];
-                acc += member_hash(seed, key, rho);
-                acc2 += member_hash(seed2, key, rho);
+                acc += member_hash(seed, key, t);
+                acc2 += member_hash(seed2, key, t);
             }
         }
 #pragma unroll
@@ -445,27 +444,15 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
     }
 }
 
-// ntail[T] = the smallest ftail over tiles T' > T (one workgroup; position
-// n - 1 ends a run, so every tile but the last has one after it)
-__global__ __launch_bounds__(1024) void k_tail_suffix(const uint32_t* __restrict__ ftail, int64_t ntiles,
-                                                     uint32_t* __restrict__ ntail) {
-    __shared__ uint32_t cm[1024];
-    const int tid = threadIdx.x;
-    const int64_t C = (ntiles + 1023) / 1024, lo = tid * C, hi = min(ntiles, lo + C);
-    uint32_t m = kNoTail;
-    for (int64_t T = lo; T < hi; ++T) m = min(m, ftail[T]);
-    cm[tid] = m;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // inclusive suffix minimum over threads
-        const uint32_t v = tid + o < 1024 ? cm[tid + o] : kNoTail;
-        __syncthreads();
-        cm[tid] = min(cm[tid], v);
-        __syncthreads();
-    }
-    uint32_t run = tid + 1 < 1024 ? cm[tid + 1] : kNoTail;
-    for (int64_t T = hi - 1; T >= lo; --T) {
-        ntail[T] = run;
-        run = min(run, ftail[T]);
+// ntail[T] = the first run end after tile T: ftail of the next tile that
+// has one (ftail grows with T; a tile without a run end lies inside a run of
+// more than 4096 entries, and runs span < 2^21 entries, so a thread looks at
+// no more than 513 tiles -- one, almost always)
+__global__ void k_tail_suffix(const uint32_t* __restrict__ ftail, int64_t ntiles, uint32_t* __restrict__ ntail) {
+    for (int64_t T = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; T < ntiles; T += (int64_t)gridDim.x * blockDim.x) {
+        int64_t u = T + 1;
+        while (u < ntiles && ftail[u] == kNoTail) ++u;
+        ntail[T] = u < ntiles ? ftail[u] : kNoTail;
     }
 }
 
@@ -512,35 +499,48 @@ __global__ __launch_bounds__(256) void k_sum_pairs(const unsigned long long* __r
 }
 
 // The G side of the run-end sort's check: sum over the lists (g, p), g in
-// [g_lo, g_hi), of h(g * P + p, rank[G_tet]) in two lanes -- one wave per
-// list (no search for an entry's list), four entries per lane in flight;
-// one atomic pair per workgroup.
+// [g_lo, g_hi), of h(g * P + p, G_tet) in two lanes.  A wave takes 64
+// consecutive lists -- one contiguous range of G_tet -- and streams it eight
+// entries per lane in flight, each entry's list found by walking the lists'
+// starts (LDS) forward from the lane's previous entry; one atomic pair per
+// workgroup.  Reads nothing of F: it runs beside the whole sort.
 __global__ __launch_bounds__(256) void k_hash_g(const int64_t* __restrict__ G_off, const int32_t* __restrict__ G_tet,
-                                                int32_t P, int32_t g_lo, int32_t g_hi,
-                                                const uint32_t* __restrict__ rank, uint64_t seed, uint64_t seed2,
+                                                int32_t P, int32_t g_lo, int32_t g_hi, uint64_t seed, uint64_t seed2,
                                                 unsigned long long* __restrict__ sum) {
+    __shared__ uint32_t pre[4][65];
     __shared__ uint64_t ws[2 * 4];
-    const int lane = threadIdx.x & 63;
-    const int64_t l_lo = (int64_t)g_lo * P, l_hi = (int64_t)g_hi * P;
-    const int64_t waves = (int64_t)gridDim.x * 4;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* pr = pre[wv];
+    const int64_t l_lo = (int64_t)g_lo * P, l_hi = (int64_t)g_hi * P, nch = (l_hi - l_lo + 63) / 64;
     uint64_t a = 0, b = 0;
-    for (int64_t l = l_lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); l < l_hi; l += waves) {
-        const int64_t e0 = G_off[l], e1 = G_off[l + 1];
-        const uint32_t key = (uint32_t)l;  // = g * P + p
-        for (int64_t k0 = e0 + lane; k0 < e1; k0 += 4 * 64) {
-            uint32_t t[4];
+    for (int64_t ch = (int64_t)blockIdx.x * 4 + wv; ch < nch; ch += (int64_t)gridDim.x * 4) {
+        const int64_t L0 = l_lo + ch * 64;
+        const int nl = (int)min<int64_t>(64, l_hi - L0);
+        const int64_t E0 = G_off[L0];
+        pr[lane] = (uint32_t)(G_off[L0 + min(lane, nl)] - E0);  // (lanes >= nl: the range's end)
+        if (lane == 0) pr[64] = (uint32_t)(G_off[L0 + nl] - E0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t total = pr[64];
+        const int32_t* gt = G_tet + E0;
+        int j = 0;
+        for (uint32_t f0 = 0; f0 < total; f0 += 8 * 64) {
+            int32_t t[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] = (uint32_t)__builtin_nontemporal_load(G_tet + min(k0 + u * 64, e1 - 1));
-            uint32_t r[4];
+            for (int u = 0; u < 8; ++u) t[u] = __builtin_nontemporal_load(gt + min(f0 + (uint32_t)(u * 64 + lane), total - 1u));
 #pragma unroll
-            for (int u = 0; u < 4; ++u) r[u] = rank[t[u]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (k0 + u * 64 < e1) {
-                    a += member_hash(seed, key, r[u]);
-                    b += member_hash(seed2, key, r[u]);
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t f = f0 + (uint32_t)(u * 64 + lane);
+                if (f < total) {
+                    while (pr[j + 1] <= f) ++j;
+                    const uint32_t key = (uint32_t)(L0 + j);  // = g * P + p
+                    a += member_hash(seed, key, (uint32_t)t[u]);
+                    b += member_hash(seed2, key, (uint32_t)t[u]);
                 }
+            }
         }
+        __builtin_amdgcn_wave_barrier();  // pr is rewritten by the next chunk
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -548,8 +548,8 @@ __global__ __launch_bounds__(256) void k_hash_g(const int64_t* __restrict__ G_of
         b += __shfl_down(b, o, 64);
     }
     if (lane == 0) {
-        ws[2 * (threadIdx.x >> 6)] = a;
-        ws[2 * (threadIdx.x >> 6) + 1] = b;
+        ws[2 * wv] = a;
+        ws[2 * wv + 1] = b;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -567,6 +567,7 @@ struct SrcFEnds {
     uint32_t P;
     int kb;
     int32_t g_lo, g_hi;
+    bool compact;  // few records kept: k_sort_scatter packs them before ranking
     __device__ __forceinline__ bool keep(uint64_t r) const { return !(r >> 63); }
     __device__ __forceinline__ uint64_t rec(int64_t i, int32_t g, int32_t p, uint32_t d) const {
         return (uint64_t)((uint32_t)g * P + (uint32_t)p) | ((uint64_t)(i & (kEndsTile - 1)) << kb) |
@@ -847,9 +848,39 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
         // the per-wave counters cleared by 16-B stores (W * BINS / 8 of them)
         for (int x = tid; x < W * BINS / 8; x += NT) reinterpret_cast<uint4*>(cnt)[x] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
+        // Src::kFilter with few records kept (a rank's genomes, pfaai_load_rows):
+        // each wave first packs its kept records, in order, into its first
+        // rounds (through its own eighth of the LDS tile, free until the
+        // reorder below), so the ranking ballots run over ceil(kept / 64)
+        // rounds instead of kSortItems; dropped slots get the drop bit
+        int kact = kSortItems;
+        if constexpr (Src::kFilter) {
+            if (src.compact) {
+                uint64_t* ws = srt + wid * (kSortItems * 64);
+                uint32_t cw = 0;
+#pragma unroll
+                for (int k = 0; k < kSortItems; ++k) {
+                    const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n && src.keep(rec[k]);
+                    const uint64_t m = __ballot(valid);
+                    if (valid) ws[cw + (uint32_t)__popcll(m & lt)] = rec[k];
+                    cw += (uint32_t)__popcll(m);
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = 0; k < kSortItems; ++k) {
+                    const uint32_t j = (uint32_t)(k * 64 + lane);
+                    rec[k] = j < cw ? ws[j] : (1ull << 63);
+                }
+                kact = (int)((cw + 63u) >> 6);
+            }
+        }
         uint16_t lr[kSortItems];
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
+            if (k >= kact) {  // (wave-uniform)
+                lr[k] = 0;
+                continue;
+            }
             const bool valid = t0 + (wid * kSortItems + k) * 64 + lane < n && src.keep(rec[k]);
             const uint32_t d = sort_digit(rec[k], shift, mask);
             uint64_t peers = __ballot(valid);
@@ -1056,8 +1087,7 @@ __global__ void k_len_from_t(const int32_t* __restrict__ T, int32_t P, int32_t n
 //         per load, so the WK 3 row kernel reads (G_pos, G_end) coalesced;
 //   HASH: the G side of the both-given check (DstGpos): sums[0] +=
 //         h(list of k, G_tet[k]) and, keyed by seed2, sums[2] (k_hash_f's
-//         second lane); with rho, h(list of k, rank of G_tet[k] among the
-//         non-empty F blocks) -- the F side then comes from k_fends_hist.
+//         second lane).
 // The lists are taken protein-major (all genomes of protein p, then p + 1),
 // so the table lookups in flight hit one or two protein rows (640 KB each),
 // which stay in every XCD's L2 -- genome-major order touched all 100 rows at
@@ -1072,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
                                               int64_t n_lists, int32_t P, const uint32_t* __restrict__ ends,
                                               uint32_t* __restrict__ G_end, uint64_t seed, uint64_t seed2,
                                               unsigned long long* __restrict__ sums, int32_t g_lo,
-                                              int32_t g_hi, const uint32_t* __restrict__ rank) {
+                                              int32_t g_hi) {
     __shared__ int64_t lb[kGendLists];
     __shared__ uint32_t pre[kGendLists + 1];
     __shared__ int64_t row[kGendLists];
@@ -1132,11 +1162,8 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
                 if (f0 + (uint32_t)u * 256u < total) {
                     if constexpr (END) G_end[k[u]] = v[u];
                     if constexpr (HASH) {
-                        // rho (the run-end sort's check): the rank of t among the non-empty F blocks
-                        uint32_t x = (uint32_t)t[u];
-                        if (rank) x = rank[x];
-                        hm += member_hash(seed, li[u], x);
-                        hm2 += member_hash(seed2, li[u], x);
+                        hm += member_hash(seed, li[u], (uint32_t)t[u]);
+                        hm2 += member_hash(seed2, li[u], (uint32_t)t[u]);
                     }
                 }
             }

@@ -22,16 +22,54 @@ from __future__ import annotations
 # (profiles/r02m_shard_times_10k_x8.txt).  Balancing by pairs alone gives
 # the last rank (narrow rows) 2.5 ms.  Round 3's row kernel (G_end, no run
 # table in the step) moved the balance toward the wide rows: 1.0 n -> 1.22,
-# 0.9 n -> 1.16, 0.8 n -> 1.16, 0.7 n -> 1.15 ms (profiles/r03o/shard_times.txt;
-# the row-profile fit gives 0.92 n); 0.8 n sits in the middle of the flat part.
-FIXED_COST_FRACTION = 0.8
+# 0.9 n -> 1.16, 0.8 n -> 1.16, 0.7 n -> 1.15 ms (profiles/r03o/shard_times.txt).
+# Round 4 (profiles/r04/shard_*.txt: 8-way shard times of seven splits, each
+# block run alone on one MI355X): the narrow rows (<= 2 047 columns) run as
+# 512-thread workgroups four per CU, so they cost less than the model said --
+# NARROW_COST_FACTOR; the cuts of the measurement-recut split (three rounds
+# of re-cutting by measured time, then a search) are met within 40 rows by
+# fixed 0.68 n and narrow rows at 0.93 of their cost.
+FIXED_COST_FRACTION = 0.68
+NARROW_COLS = 2047
+NARROW_COST_FACTOR = 0.93
+# A shard of m rows runs in rounds of 2 x CUs workgroups (two 1024-thread
+# row workgroups per CU), and a round's few last rows cost about half a row
+# time whatever their number: at 10k x 8, 1 022 rows measured 0.95 ms and
+# 1 029 or 1 044 rows 1.17-1.20 ms for neighbouring blocks (a mean of 1.10).
+# With cus given, a cut that leaves a block up to ROUND_TAIL of a round past
+# a whole number of rounds moves back to the round boundary (its rows go to
+# the next block), and so does a cut up to ROUND_TAIL of a round past the
+# first narrow row.
+ROUND_TAIL = 0.25
 
 
-def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: float | None = None):
+def split_rows(n_rows: int, world: int, all_vs_all: bool = True, fixed_cols: float | None = None,
+               cus: int | None = None):
     """-> [(row_begin, row_end)] * world, contiguous, covering [0, n_rows),
-    balanced by the row cost model fixed_cols + width (all-vs-all row a has
-    width n-1-a; QT/QSUB rows are equal)."""
-    return split_range(0, n_rows, world, n_rows, all_vs_all, fixed_cols)
+    balanced by the row cost model (row_costs: fixed + width for all-vs-all
+    row a of width n-1-a, narrow rows scaled; QT/QSUB rows are equal).
+    cus (the GPU's compute units): cuts that leave a block a few rows into
+    another round of 2 * cus workgroups move back to the round boundary."""
+    blocks = split_range(0, n_rows, world, n_rows, all_vs_all, fixed_cols)
+    if not (cus and all_vs_all and world > 1):
+        return blocks
+    S = 2 * int(cus)
+    edges = [0]
+    for k, (_, b) in enumerate(blocks[:-1]):
+        a = edges[-1]
+        m = b - a
+        tail = m % S
+        if m > S and 0 < tail <= ROUND_TAIL * S and n_rows - 1 - (b - 1) > NARROW_COLS:
+            b -= tail
+        # a cut a few rows past the first narrow row moves back to it: the
+        # block's narrow rows would run as their own small launch beside its
+        # wide ones (10k x 8: [6460, 7988) 1.11-1.14 ms, [6421, 7952) 1.05-1.06)
+        narrow0 = n_rows - 1 - NARROW_COLS
+        if 0 < b - narrow0 <= ROUND_TAIL * S:
+            b = narrow0
+        edges.append(max(a, b))
+    edges.append(n_rows)
+    return [(edges[i], edges[i + 1]) for i in range(world)]
 
 
 def split_range(row_lo: int, row_hi: int, parts: int, n_rows: int, all_vs_all: bool = True,
@@ -41,24 +79,14 @@ def split_range(row_lo: int, row_hi: int, parts: int, n_rows: int, all_vs_all: b
     if not all_vs_all:
         cuts = [row_lo + (row_hi - row_lo) * r // parts for r in range(parts + 1)]
         return [(cuts[i], cuts[i + 1]) for i in range(parts)]
-    n = n_rows
-    k = FIXED_COST_FRACTION * n if fixed_cols is None else float(fixed_cols)
+    import numpy as np
 
-    def before(a):  # cost of rows < a: a fixed parts + the pairs of the upper triangle
-        return a * k + a * n - a * (a + 1) // 2
-
-    c0, c1 = before(row_lo), before(row_hi)
+    cum = np.concatenate([[0.0], np.cumsum(row_costs(n_rows, True, fixed_cols))])
+    c0, c1 = cum[row_lo], cum[row_hi]
     cuts = [row_lo]
     for r in range(1, parts):
         target = c0 + (c1 - c0) * r / parts
-        lo, hi = cuts[-1], row_hi
-        while lo < hi:
-            mid = (lo + hi) // 2
-            if before(mid) < target:
-                lo = mid + 1
-            else:
-                hi = mid
-        cuts.append(lo)
+        cuts.append(int(min(max(np.searchsorted(cum, target, side="left"), cuts[-1]), row_hi)))
     cuts.append(row_hi)
     return [(cuts[i], cuts[i + 1]) for i in range(parts)]
 
@@ -72,7 +100,11 @@ def row_costs(n_rows: int, all_vs_all: bool = True, fixed_cols: float | None = N
     if not all_vs_all:
         return np.ones(n_rows)
     k = FIXED_COST_FRACTION * n_rows if fixed_cols is None else float(fixed_cols)
-    return k + (n_rows - 1 - np.arange(n_rows, dtype=np.float64))
+    width = n_rows - 1 - np.arange(n_rows, dtype=np.float64)
+    c = k + width
+    if fixed_cols is None:  # (an explicit fixed cost: the plain model)
+        c[width <= NARROW_COLS] *= NARROW_COST_FACTOR
+    return c
 
 
 class PipelinedGather:

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from parfastaai_amd.shard import FIXED_COST_FRACTION, split_rows
+from parfastaai_amd.shard import FIXED_COST_FRACTION, NARROW_COLS, NARROW_COST_FACTOR, ROUND_TAIL, row_costs, split_rows
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -64,10 +64,25 @@ def test_split_rows_balanced():
         blocks = split_rows(n, w)
         assert blocks[0][0] == 0 and blocks[-1][1] == n
         assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
-        k = FIXED_COST_FRACTION * n
-        cost = [sum(k + n - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]
+        c = row_costs(n)
+        cost = [c[b0:b1].sum() for b0, b1 in blocks]
         if n >= 100 * w:
-            assert max(cost) - min(cost) <= 2 * (k + n)  # within a row or two
+            assert max(cost) - min(cost) <= 2 * (FIXED_COST_FRACTION * n + n)  # within a row or two
+    # the model: fixed + width, narrow rows (<= NARROW_COLS columns) scaled
+    c = row_costs(5000)
+    assert c[0] == FIXED_COST_FRACTION * 5000 + 4999
+    assert c[-1] == NARROW_COST_FACTOR * FIXED_COST_FRACTION * 5000
+    # cus: a cut a few rows into another round of 2 * cus workgroups moves back
+    plain = split_rows(10000, 8)
+    rounded = split_rows(10000, 8, cus=256)
+    assert rounded[0][0] == 0 and rounded[-1][1] == 10000
+    assert all(rounded[i][1] == rounded[i + 1][0] for i in range(7))
+    for (b0, b1), (p0, p1) in zip(rounded, plain):
+        m = b1 - b0
+        if 10000 - b1 > NARROW_COLS + 1 and m > 512:
+            assert not 0 < m % 512 <= ROUND_TAIL * 512, (b0, b1)
+    assert rounded != plain  # (the 10k x 8 plain split leaves block 3 66 rows into a third round)
+    assert split_rows(10, 3, cus=256) == split_rows(10, 3)
     # pure pair balance with fixed_cols = 0
     blocks = split_rows(10000, 8, fixed_cols=0)
     pairs = [sum(10000 - 1 - a for a in range(b0, b1)) for b0, b1 in blocks]

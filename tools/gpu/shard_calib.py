@@ -4,7 +4,9 @@ rounds of re-cutting by the measured cost (each block's measured time
 spread over its rows in proportion to the model cost, the cuts moved to
 equal shares), and the model's fit to the final cuts.
 
-    python tools/gpu/shard_calib.py [n] [world] [rounds]
+    python tools/gpu/shard_calib.py [n] [world] [rounds] [--cuts c1,c2,...;c1,c2,...]
+
+--cuts: time these splits (each twice) instead of the re-cutting rounds.
 """
 import json
 import os
@@ -18,6 +20,11 @@ from parfastaai_amd import _capi, syn  # noqa: E402
 from parfastaai_amd.datastruct import ParFAAIData  # noqa: E402
 from parfastaai_amd.shard import row_costs, split_rows  # noqa: E402
 
+cut_sets = None
+if "--cuts" in sys.argv:
+    k = sys.argv.index("--cuts")
+    cut_sets = [[int(x) for x in cs.split(",")] for cs in sys.argv[k + 1].split(";")]
+    del sys.argv[k:k + 2]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 world = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
@@ -50,7 +57,15 @@ def report(label, blocks, ms):
                       "max_over_mean": round(max(ms) / float(np.mean(ms)), 4)}), flush=True)
 
 
-blocks = split_rows(rows, world)
+if cut_sets:
+    for rep in range(2):
+        for cs in cut_sets:
+            edges = [0] + cs + [rows]
+            blocks = [(edges[i], edges[i + 1]) for i in range(len(edges) - 1)]
+            report(f"cuts rep {rep}", blocks, times(blocks))
+    eng.free(d)
+    sys.exit(0)
+blocks = split_rows(rows, world, cus=torch.cuda.get_device_properties(0).multi_processor_count)
 ms = times(blocks)
 report("model", blocks, ms)
 w = row_costs(rows)  # the model's per-row cost
