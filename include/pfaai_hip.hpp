@@ -90,8 +90,10 @@ void par_range(int64_t n, Fn fn) {
 
 // Contiguous row blocks over `parts` devices: cut[0] = 0 .. cut[parts] = n,
 // balanced by the row-cost model of parfastaai_amd/shard.py:split_rows (the
-// same cuts, pinned by tests/test_integration_compile.py): all-vs-all row a
-// costs fixed + width = 1.0 n + (n - 1 - a); QT / QSUB rows are equal.
+// same cuts, pinned by tests/test_adapter_split.py): all-vs-all row a costs
+// fixed + width = 0.68 n + (n - 1 - a), times 0.93 for the narrow rows (width
+// <= 2047, the 512-thread launch); QT / QSUB rows are equal.  The prefix sums
+// are accumulated in row order in double, as numpy's cumsum does.
 inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
     std::vector<int64_t> cut{0};
     if (!all_vs_all) {
@@ -99,17 +101,19 @@ inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
         cut.push_back(n);
         return cut;
     }
-    const double k = 0.8 * (double)n;  // shard.FIXED_COST_FRACTION
-    auto before = [&](int64_t a) { return (double)a * k + (double)a * n - (double)(a * (a + 1) / 2); };
-    const double total = before(n);
+    const double k = 0.68 * (double)n;  // shard.FIXED_COST_FRACTION
+    std::vector<double> cum((size_t)n + 1, 0.0);
+    for (int64_t a = 0; a < n; ++a) {
+        const double width = (double)(n - 1 - a);
+        double c = k + width;
+        if (width <= 2047.0) c *= 0.93;  // shard.NARROW_COLS, NARROW_COST_FACTOR
+        cum[(size_t)a + 1] = cum[(size_t)a] + c;
+    }
+    const double total = cum[(size_t)n];
     for (int r = 1; r < parts; ++r) {
-        int64_t lo = cut.back(), hi = n;
-        const double target = total * r / parts;
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) / 2;
-            if (before(mid) < target) lo = mid + 1; else hi = mid;
-        }
-        cut.push_back(lo);
+        const double target = 0.0 + (total - 0.0) * r / parts;
+        int64_t i = std::lower_bound(cum.begin(), cum.end(), target) - cum.begin();
+        cut.push_back(std::min<int64_t>(std::max<int64_t>(i, cut.back()), n));
     }
     cut.push_back(n);
     return cut;

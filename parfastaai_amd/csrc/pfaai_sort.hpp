@@ -33,6 +33,7 @@
 // checks them -- instead of a sorted copy.
 #pragma once
 #include "pfaai_kernels.hpp"
+#include "pfaai_util.hpp"
 
 namespace pfaai {
 
@@ -332,26 +333,31 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
         stz[tid] = tnz[ix < (unsigned long long)kNTetramers ? (int64_t)ix : (int64_t)kNTetramers - 1];
     }
     for (int b = tid; b < BINS; b += NT) h[b] = 0u;
+    // tile-relative 32-bit positions (rn: the tile's entries, uniform) -- the
+    // VALU-bound kernel (~110 VALU per entry with 64-bit positions) keeps its
+    // address arithmetic in the scalar base
+    // (raw buffer loads / stores over the tile: out-of-range positions read
+    // 0 and write nothing, so no clamps or branches per entry)
+    const int rn = (int)min<int64_t>(kTile, n - t0);
+    const rsrc_t r_p = mk_rsrc(Fp + t0, (uint64_t)rn * 4u), r_g = mk_rsrc(Fg + t0, (uint64_t)rn * 4u);
+    const rsrc_t r_fp16 = mk_rsrc(fp16 ? fp16 + t0 : nullptr, fp16 ? (uint64_t)rn * 2u : 0u);
+    const uint32_t gspan = (uint32_t)(g_hi - g_lo);
     int32_t p[kSortItems], g[kSortItems];
 #pragma unroll
     for (int k = 0; k < kSortItems; ++k) {
-        const int64_t i = min(t0 + (int64_t)(k * NT + tid), n - 1);
-        p[k] = __builtin_nontemporal_load(Fp + i);
-        g[k] = __builtin_nontemporal_load(Fg + i);
+        p[k] = (int32_t)bld_u32(r_p, (uint32_t)(k * NT + tid) * 4u, 0u);
+        g[k] = (int32_t)bld_u32(r_g, (uint32_t)(k * NT + tid) * 4u, 0u);
     }
-    const int64_t nw = (n + 31) >> 5;
-    const uint32_t bw = tid < kTile / 32 ? bend[min(t0 / 32 + tid, nw - 1)] : 0u;
+    const int nwt = (int)min<int64_t>(kTile / 32, ((n + 31) >> 5) - t0 / 32);  // bend words of the tile
+    const uint32_t bw = tid < nwt ? bend[t0 / 32 + tid] : 0u;
     const int32_t p_next = t0 + kTile < n ? Fp[t0 + kTile] : -1;
     __syncthreads();  // (h cleared)
 #pragma unroll
     for (int k = 0; k < kSortItems; ++k) {
         const int r = k * NT + tid;
-        const int64_t i = t0 + r;
         sp[r] = (uint16_t)p[k];
-        if (i < n) {
-            if (fp16) fp16[i] = (uint16_t)p[k];
-            if (g[k] >= g_lo && g[k] < g_hi) atomicAdd(&h[((uint32_t)g[k] * P + (uint32_t)p[k]) & mask], 1u);
-        }
+        if (fp16) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)p[k], r_fp16, r * 2, 0, 0);
+        if (r < rn && (uint32_t)(g[k] - g_lo) < gspan) atomicAdd(&h[((uint32_t)g[k] * P + (uint32_t)p[k]) & mask], 1u);
     }
     if (tid < kTile / 32) sb[tid] = bw;
     if (tid == 0) sp[kTile] = (uint16_t)p_next;  // (-1: 0xFFFF, no protein id)
@@ -372,12 +378,10 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
             const int r = k * NT + tid;
-            const int64_t i = t0 + r;
             const uint32_t w = (uint32_t)r >> 5;
-            const uint32_t rho = (uint32_t)rb + wpre[w] + (w >= 64 ? carry : 0u) + __popc(sb[w] & ((1u << (r & 31)) - 1u));
-            const uint32_t rl = rho - (uint32_t)rb;
-            const uint32_t t = rl < 64u ? stz[rl] : tnz[i < n ? rho : 0u];
-            if (i < n && g[k] >= g_lo && g[k] < g_hi) {
+            const uint32_t rl = wpre[w] + (w >= 64 ? carry : 0u) + __popc(sb[w] & ((1u << (r & 31)) - 1u));
+            const uint32_t t = rl < 64u ? stz[rl] : tnz[r < rn ? (uint32_t)rb + rl : 0u];
+            if (r < rn && (uint32_t)(g[k] - g_lo) < gspan) {
                 const uint32_t key = (uint32_t)g[k] * P + (uint32_t)p[k];
                 acc += member_hash(seed, key, t);
                 acc2 += member_hash(seed2, key, t);
@@ -405,8 +409,7 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
 #pragma unroll 1
     for (int k = 0; k < kSortItems; ++k) {  // run ends, one 64-position chunk per (wave, k) ballot
         const int r = k * NT + tid;
-        const int64_t i = t0 + r;
-        const bool tail = i < n && (i == n - 1 || ((sb[r >> 5] >> (r & 31)) & 1u) || sp[r] != sp[r + 1]);
+        const bool tail = r < rn && (t0 + r == n - 1 || ((sb[r >> 5] >> (r & 31)) & 1u) || sp[r] != sp[r + 1]);
         const unsigned long long m = __ballot(tail);
         if (lane == 0) tm[r >> 6] = m;
     }
@@ -424,6 +427,7 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
     }
     __syncthreads();
     for (int b = tid; b < BINS; b += NT) hist[tile * BINS + b] = h[b];
+    const rsrc_t r_d = mk_rsrc(D + t0, (uint64_t)rn * 4u);
     if (tid == 0) {
         ftail[tile] = first == kNoTail ? kNoTail : (uint32_t)(t0 + first);
         ltail[tile] = last;  // (tile-relative: the tile's open run starts after it)
@@ -440,7 +444,7 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
             const uint32_t w2 = nextw[w];
             if (w2 < (uint32_t)kChunks) d = (w2 << 6) + (uint32_t)__builtin_ctzll(tm[w2]) + 1u - r;
         }
-        if (t0 + r < n) D[t0 + r] = d;
+        __builtin_amdgcn_raw_buffer_store_b32(d, r_d, (int)(r * 4u), 0, 0);
     }
 }
 
@@ -745,7 +749,7 @@ constexpr int sort_scatter_wpe() { return NT == 512 ? 4 : 1; }
 // PF: the next tile's records and digit bases are loaded while this tile is
 // ranked and written (16 + BPT VGPRs live across the tile)
 // VAR (diagnostics A/B, 0 in the product): bit 0 round-robin tile order,
-// bit 1 the ranking ballots done twice (their cost), bit 3 no global stores
+// bit 3 no global stores
 // (ablation), bit 4 ordinary (temporal) record loads, bit 5 a static tile
 // stride instead of the per-XCD tile counters (tctr[8], zeroed by k_sort_top)
 template <int DB, int NT, bool PF, class Src, class Dst, int VAR = 0>
@@ -874,7 +878,60 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
                 kact = (int)((cw + 63u) >> 6);
             }
         }
+        // ranking: peers = the valid lanes with this item's digit.  Two
+        // forms.  kPairRank (the run-end sort's first pass, SrcFEnds): peers
+        // accumulated as its complement, the lanes that differ in some bit --
+        // per bit the bit as 0 / -1 (one v_bfe_i32), its ballot, and diff |=
+        // ballot ^ bit in each half (one v_bitop3 each), 4 VALU per bit where
+        // peers &= on ? m : ~m takes 8 (a 0 / -1 select, two xors, two ands,
+        // the bit extracted twice); two items at a time, their bits
+        // interleaved (a ballot's SGPR read by the next VALU op waits
+        // otherwise).  Pass 1 of the 10k load 2.13 -> 1.85 ms; the same form
+        // in pass 2 (SrcRecs -> DstGposEnds) measured 1.93 -> 2.17-2.21 ms,
+        // so the other sources keep the first form.
+        constexpr bool kPairRank = Src::kFilter;
         uint16_t lr[kSortItems];
+        static_assert(kSortItems % 2 == 0, "items in pairs");
+        if constexpr (kPairRank) {
+#pragma unroll
+        for (int k = 0; k < kSortItems; k += 2) {
+            if (k >= kact) {  // (wave-uniform; kact is odd only when the wave packed its kept records)
+                lr[k] = 0;
+                lr[k + 1] = 0;
+                continue;
+            }
+            bool valid[2];
+            uint32_t d[2], dlo[2], dhi[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                valid[u] = k + u < kact && t0 + (wid * kSortItems + k + u) * 64 + lane < n && src.keep(rec[k + u]);
+                d[u] = sort_digit(rec[k + u], shift, mask);
+                const uint64_t vm = __ballot(valid[u]);
+                dlo[u] = ~(uint32_t)vm;
+                dhi[u] = ~(uint32_t)(vm >> 32);
+            }
+#pragma unroll
+            for (int bit = 0; bit < DB; ++bit) {  // (bits above the mask are 0 in every lane: same ballot)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    uint32_t rep = (uint32_t)__builtin_amdgcn_sbfe((int)d[u], bit, 1);
+                    asm("" : "+v"(rep));  // (opaque: the ballot compares rep, not a re-shifted d)
+                    const uint64_t m = __ballot(rep != 0u);
+                    // dx | (m ^ rep): LUT 0xF6 over (dx, m, rep)
+                    dlo[u] = __builtin_amdgcn_bitop3_b32(dlo[u], (uint32_t)m, rep, 0xF6);
+                    dhi[u] = __builtin_amdgcn_bitop3_b32(dhi[u], (uint32_t)(m >> 32), rep, 0xF6);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint64_t peers = ~(((uint64_t)dhi[u] << 32) | dlo[u]);
+                const uint32_t r = (uint32_t)__popcll(peers & lt), c = (uint32_t)__popcll(peers);
+                const uint32_t base = valid[u] ? wc[d[u]] : 0u;
+                lr[k + u] = (uint16_t)(base + r);
+                if (valid[u] && r + 1 == c) wc[d[u]] = (uint16_t)(base + c);  // the group's last lane advances the counter
+            }
+        }
+        } else {
 #pragma unroll
         for (int k = 0; k < kSortItems; ++k) {
             if (k >= kact) {  // (wave-uniform)
@@ -890,22 +947,11 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
                 const uint64_t m = __ballot(on);
                 peers &= on ? m : ~m;
             }
-            if constexpr ((VAR & 2) != 0) {  // the ballots a second time (their cost, by difference)
-                uint64_t p2 = __ballot(valid);
-                uint32_t d2 = d;
-                asm volatile("" : "+v"(d2));  // opaque: the ballots are not folded into the first set
-#pragma unroll
-                for (int bit = 0; bit < DB; ++bit) {
-                    const bool on = (d2 >> bit) & 1u;
-                    const uint64_t m = __ballot(on);
-                    p2 &= on ? m : ~m;
-                }
-                peers = p2;
-            }
             const uint32_t r = (uint32_t)__popcll(peers & lt), c = (uint32_t)__popcll(peers);
             const uint32_t base = valid ? wc[d] : 0u;
             lr[k] = (uint16_t)(base + r);
             if (valid && r + 1 == c) wc[d] = (uint16_t)(base + c);  // the group's last lane advances the counter
+        }
         }
         __syncthreads();
         // per digit: the waves' counts -> exclusive prefix over waves; the
