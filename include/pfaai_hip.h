@@ -22,7 +22,8 @@
  *   - no C++ exception crosses the ABI (allocation failures -> PFAAI_RC_OOM).
  *   - host inputs are borrowed for the duration of the call; device buffers
  *     are owned by the context; outputs are caller-owned.
- *   - one host thread drives one context; a context owns one device.
+ *   - one host thread drives one context; a context owns one device (a
+ *     pfaai_group owns several, with an RCCL communicator over them).
  */
 #ifndef PFAAI_HIP_H
 #define PFAAI_HIP_H
@@ -33,8 +34,10 @@
 extern "C" {
 #endif
 
-#define PFAAI_ABI_VERSION 4 /* 4: F or G built on the device at load, pfaai_run_info,
-                                 PFAAI_RC_* names, dense row matrices (pfaai_stream_matrix) */
+#define PFAAI_ABI_VERSION 5 /* 4: F or G built on the device at load, pfaai_run_info,
+                                 PFAAI_RC_* names, dense row matrices (pfaai_stream_matrix);
+                                 5: pfaai_load_rows, pfaai_run_walk, the multi-device
+                                 group with its RCCL communicator (pfaai_group_*) */
 #define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
 
 /* Error codes: 0..3 have PFAAI_ERROR_CODE's values (interface.hpp:39-44). */
@@ -231,6 +234,35 @@ int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
  * adapter's multi-device constructor).  QSUB: all rows only. */
 int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
                        double* h_aji, double* h_S, int32_t* h_N);
+
+/* ---- multi-device group (pfaai_create over a device list, the
+ * RCCL communicator inside) -------------------------------------------------
+ * The device-side counterpart of distributeGenomePairs (algorithm_impl.hpp:
+ * 100-120) in one process: one context per device, one RCCL communicator
+ * over them (ncclCommInitAll), one stream per device; one host thread drives
+ * the group.  pfaai_group_load loads the caller's host arrays on every
+ * device concurrently (one host copy feeds all of them) and builds each
+ * device's walk data for its own row block only (pfaai_load_rows); blocks
+ * by the row-cost model of pfaai::split_rows (pfaai_hip.hpp) for ALL, equal
+ * rows for QT; a QSUB problem runs on the first device alone (its rows'
+ * JAC spans are not contiguous).  pfaai_group_run computes every block on
+ * its device and gathers them into the caller's arrays on the FIRST device
+ * (device_ids[0]; length n_pairs, JAC index order) by grouped ncclSend /
+ * ncclRecv over xGMI; synchronous.  d_S / d_N are required with
+ * PFAAI_FLAG_EMIT_JAC; PFAAI_FLAG_FULL_ROWS is not supported here.
+ * Errors: PFAAI_RC_INVALID for a bad or repeated device id, PFAAI_RC_RCCL
+ * for a communicator failure; pfaai_group_last_error gives the message. */
+typedef struct pfaai_group pfaai_group;
+int pfaai_group_create(pfaai_group** group, const int* device_ids, int n_devices);
+int pfaai_group_destroy(pfaai_group* group);
+const char* pfaai_group_last_error(const pfaai_group* group);
+int pfaai_group_size(const pfaai_group* group, int* n_devices);
+/* the context of device_ids[i] (stats, timing, row spans); owned by the group */
+pfaai_ctx* pfaai_group_ctx(pfaai_group* group, int i);
+int pfaai_group_load(pfaai_group* group, const pfaai_problem* prob);
+/* the row blocks of the loaded problem: cuts[0] = 0 .. cuts[n_devices] = rows */
+int pfaai_group_blocks(const pfaai_group* group, int64_t* cuts);
+int pfaai_group_run(pfaai_group* group, uint32_t flags, double* d_aji, double* d_S, int32_t* d_N);
 
 /* Times (ms) of the last pfaai_load: host-side checks and H2D copies (wall),
  * and the device span of the F / G build (or G-covers-F check), HIP events

@@ -39,6 +39,8 @@ EXPORTS = [
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
     "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_rows", "pfaai_load_timing", "pfaai_stream_matrix",
     "pfaai_load_info",
+    "pfaai_group_create", "pfaai_group_destroy", "pfaai_group_last_error", "pfaai_group_size", "pfaai_group_ctx",
+    "pfaai_group_load", "pfaai_group_blocks", "pfaai_group_run",
 ]
 LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
@@ -117,6 +119,14 @@ def load_library(path=None):
         "pfaai_load_info": (ctypes.c_int, [vp, ctypes.POINTER(i32)]),
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
+        "pfaai_group_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+        "pfaai_group_destroy": (ctypes.c_int, [vp]),
+        "pfaai_group_last_error": (ctypes.c_char_p, [vp]),
+        "pfaai_group_size": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+        "pfaai_group_ctx": (vp, [vp, ctypes.c_int]),
+        "pfaai_group_load": (ctypes.c_int, [vp, ctypes.POINTER(Problem)]),
+        "pfaai_group_blocks": (ctypes.c_int, [vp, P64]),
+        "pfaai_group_run": (ctypes.c_int, [vp, u32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -127,6 +137,27 @@ def load_library(path=None):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _problem(*, mode, n_ids, n_prot, T, Lp=None, F_prot=None, F_genome=None, n_qry=0, n_tgt=0, is_q=None,
+             q_index=None, t_rank=None, G_off=None, G_tet=None):
+    """-> (pfaai_problem, the contiguous arrays it points into: keep them alive)"""
+    Lp = None if Lp is None else np.ascontiguousarray(Lp, dtype=np.int64)
+    F_prot = None if F_prot is None else np.ascontiguousarray(F_prot, dtype=np.int32)
+    F_genome = None if F_genome is None else np.ascontiguousarray(F_genome, dtype=np.int32)
+    T = np.ascontiguousarray(T, dtype=np.int32)
+    is_q = None if is_q is None else np.ascontiguousarray(is_q, dtype=np.uint8)
+    q_index = None if q_index is None else np.ascontiguousarray(q_index, dtype=np.int32)
+    t_rank = None if t_rank is None else np.ascontiguousarray(t_rank, dtype=np.int32)
+    G_off = None if G_off is None else np.ascontiguousarray(G_off, dtype=np.int64)
+    G_tet = None if G_tet is None else np.ascontiguousarray(G_tet, dtype=np.int32)
+    assert Lp is None or Lp.shape == (NTETRAMERS + 1,)
+    assert T.ndim == 2 and T.shape[0] == n_prot
+    pb = Problem(mode=mode, n_ids=n_ids, n_prot=n_prot, t_cols=T.shape[1], n_qry=n_qry,
+                 n_tgt=n_tgt, n_f=0 if F_prot is None else F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
+                 F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
+                 t_rank=_ptr(t_rank), G_off=_ptr(G_off), G_tet=_ptr(G_tet))
+    return pb, (Lp, F_prot, F_genome, T, is_q, q_index, t_rank, G_off, G_tet)
 
 
 class Engine:
@@ -163,21 +194,9 @@ class Engine:
         missing is built on the device (pfaai_load).  rows=(begin, end): the
         output rows this context will run (pfaai_load_rows: a rank's block;
         the all-vs-all walk data is built for those rows only)."""
-        Lp = None if Lp is None else np.ascontiguousarray(Lp, dtype=np.int64)
-        F_prot = None if F_prot is None else np.ascontiguousarray(F_prot, dtype=np.int32)
-        F_genome = None if F_genome is None else np.ascontiguousarray(F_genome, dtype=np.int32)
-        T = np.ascontiguousarray(T, dtype=np.int32)
-        is_q = None if is_q is None else np.ascontiguousarray(is_q, dtype=np.uint8)
-        q_index = None if q_index is None else np.ascontiguousarray(q_index, dtype=np.int32)
-        t_rank = None if t_rank is None else np.ascontiguousarray(t_rank, dtype=np.int32)
-        G_off = None if G_off is None else np.ascontiguousarray(G_off, dtype=np.int64)
-        G_tet = None if G_tet is None else np.ascontiguousarray(G_tet, dtype=np.int32)
-        assert Lp is None or Lp.shape == (NTETRAMERS + 1,)
-        assert T.ndim == 2 and T.shape[0] == n_prot
-        pb = Problem(mode=mode, n_ids=n_ids, n_prot=n_prot, t_cols=T.shape[1], n_qry=n_qry,
-                     n_tgt=n_tgt, n_f=0 if F_prot is None else F_prot.shape[0], Lp=_ptr(Lp), F_prot=_ptr(F_prot),
-                     F_genome=_ptr(F_genome), T=_ptr(T), is_q=_ptr(is_q), q_index=_ptr(q_index),
-                     t_rank=_ptr(t_rank), G_off=_ptr(G_off), G_tet=_ptr(G_tet))
+        pb, keep = _problem(mode=mode, n_ids=n_ids, n_prot=n_prot, T=T, Lp=Lp, F_prot=F_prot,
+                            F_genome=F_genome, n_qry=n_qry, n_tgt=n_tgt, is_q=is_q, q_index=q_index,
+                            t_rank=t_rank, G_off=G_off, G_tet=G_tet)  # (keep: borrowed for the call only)
         if rows is None:
             self._check(self.lib.pfaai_load(self.ctx, ctypes.byref(pb)), "pfaai_load")
         else:
@@ -349,3 +368,58 @@ class Engine:
         out = np.empty(count, dtype=dtype)
         self._check(self.lib.pfaai_memcpy_d2h(self.ctx, _ptr(out), ptr, out.nbytes), "pfaai_memcpy_d2h")
         return out
+
+
+class Group:
+    """pfaai_group: several devices in one process, one RCCL communicator
+    over them.  load() puts the problem on every device (each
+    builds the walk data of its own row block); run() computes every block
+    and gathers them into device-0 arrays (grouped ncclSend / ncclRecv)."""
+
+    def __init__(self, devices, lib_path=None):
+        self.lib = load_library(lib_path)
+        self.g = ctypes.c_void_p()
+        ids = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        rc = self.lib.pfaai_group_create(ctypes.byref(self.g), ids, len(devices))
+        if rc != PFAAI_OK:
+            raise PfaaiError(rc, f"pfaai_group_create(devices={list(devices)})")
+        self.n = len(devices)
+        self._keep = None
+
+    def _check(self, rc, what):
+        if rc != PFAAI_OK:
+            msg = self.lib.pfaai_group_last_error(self.g)
+            raise PfaaiError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self.g:
+            self.lib.pfaai_group_destroy(self.g)
+            self.g = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, **kw):
+        pb, keep = _problem(**kw)  # (keep: borrowed for the call only)
+        self._check(self.lib.pfaai_group_load(self.g, ctypes.byref(pb)), "pfaai_group_load")
+        del keep
+
+    def blocks(self):
+        cuts = (ctypes.c_int64 * (self.n + 1))()
+        self._check(self.lib.pfaai_group_blocks(self.g, cuts), "pfaai_group_blocks")
+        return [(cuts[i], cuts[i + 1]) for i in range(self.n)]
+
+    def shape(self):
+        r, p = ctypes.c_int64(), ctypes.c_int64()
+        ctx = self.lib.pfaai_group_ctx(self.g, 0)
+        rc = self.lib.pfaai_shape(ctx, ctypes.byref(r), ctypes.byref(p))
+        if rc != PFAAI_OK:
+            raise PfaaiError(rc, "pfaai_shape")
+        return r.value, p.value
+
+    def run(self, flags, d_aji, d_S=None, d_N=None):
+        """Device pointers on the group's first device, length n_pairs; synchronous."""
+        self._check(self.lib.pfaai_group_run(self.g, flags, d_aji, d_S, d_N), "pfaai_group_run")

@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert _capi.load_library().pfaai_version() == 4
+    assert _capi.load_library().pfaai_version() == 5
 
 
 def test_problem_struct_layout():

@@ -64,7 +64,7 @@ def build_hip(force=False, diag=False):
         futs = [ex.submit(_run, [HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)]) for u, o in zip(units, objs)]
         for f in futs:
             f.result()  # re-raises a failed compile
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs, "-ldl"])
     return out
 
 
