@@ -255,6 +255,7 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
             bool valid = false;
             uint32_t key = 0;
             uint2 rec = make_uint2(0u, 0u);
+            unsigned long long fk = ~0ull;  // FIRST: this lane's candidate
             if (i < e) {
                 const int32_t a = d.Fg[i];
                 const int32_t row = d.row_of[a];
@@ -289,10 +290,21 @@ __global__ __launch_bounds__(kTetraThreads) void k_entries(
                             }
                         }
                         if (b >= 0)
-                            atomicMin(first_key, ((unsigned long long)a << 42) | ((unsigned long long)b << 21) |
-                                                     (unsigned long long)p);
+                            fk = ((unsigned long long)a << 42) | ((unsigned long long)b << 21) | (unsigned long long)p;
                     }
                 }
+            }
+            if constexpr (FIRST) {
+                // one atomic per wave, and only if it lowers the minimum: an
+                // atomicMin per F entry on the one address serialised at the
+                // L2 (C2's 5.8e7 entries: 11 ms inside the CLI's compat run)
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long v = __shfl_xor(fk, o, 64);
+                    fk = v < fk ? v : fk;
+                }
+                if (lane == 0 && fk != ~0ull && fk < __hip_atomic_load(first_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    atomicMin(first_key, fk);
             }
             // compaction at this tetramer's offset (per-tetramer counts, scanned)
             const unsigned long long m = __ballot(valid);

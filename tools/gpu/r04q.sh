@@ -1,7 +1,8 @@
 #!/bin/bash
-# the group API (RCCL communicator, one rank on this box) + the ABI tests
+# the whole GPU suite (group API included) + the CLI at C2 (ours only, phases)
 set -o pipefail
 O=gpurun_out/r04q
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_group.py tests/test_gpu_load_rows.py > $O/tests.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 &&
+timeout -k 10 600 python -u tools/gpu/shard_calib.py 10000 8 0 --cuts "894,1841,2851,3875,5132,6460,7952;908,1866,2879,3901,5165,6421,7952" > $O/shard_cuts.txt 2>&1
