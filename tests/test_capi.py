@@ -46,6 +46,14 @@ def test_no_silent_cpu_fallback_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(_capi.PfaaiError):
         _capi.Engine(0)
+    # the multi-device group: no device -> a HIP error, never a host fallback;
+    # an empty device list is refused before the runtime is asked
+    with pytest.raises(_capi.PfaaiError) as e:
+        _capi.Group([0])
+    assert e.value.code == 4  # PFAAI_RC_HIP
+    with pytest.raises(_capi.PfaaiError) as e:
+        _capi.Group([])
+    assert e.value.code == 7  # PFAAI_RC_INVALID
 
 
 def test_product_does_not_import_oracle():

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Kernel statistics from a rocprofv3 --kernel-trace database (rocpd SQLite,
-the tool's default output on this image): per kernel the number of
+the tool's default output on this image) or its CSV kernel trace
+(`--output-format csv`: <prefix>_kernel_trace.csv): per kernel the number of
 dispatches and the mean / median / min / max duration, and optionally the
 dispatch sequence of one load or step (--timeline).
 
@@ -28,6 +29,12 @@ def short(name):
 
 
 def dispatches(db):
+    if db.endswith(".csv"):  # rocprofv3 --output-format csv: <prefix>_kernel_trace.csv
+        with open(db) as f:
+            rows = list(csv.DictReader(f))
+        out = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Stream_Id"]))
+               for r in rows]
+        return sorted(out, key=lambda d: d[1])
     con = sqlite3.connect(db)
     names = {r[0]: r[1] for r in con.execute("select id, kernel_name from rocpd_info_kernel_symbol")}
     rows = con.execute("select kernel_id, start, end, stream_id from rocpd_kernel_dispatch order by start").fetchall()
