@@ -34,10 +34,11 @@
 extern "C" {
 #endif
 
-#define PFAAI_ABI_VERSION 5 /* 4: F or G built on the device at load, pfaai_run_info,
+#define PFAAI_ABI_VERSION 6 /* 4: F or G built on the device at load, pfaai_run_info,
                                  PFAAI_RC_* names, dense row matrices (pfaai_stream_matrix);
                                  5: pfaai_load_rows, pfaai_run_walk, the multi-device
-                                 group with its RCCL communicator (pfaai_group_*) */
+                                 group with its RCCL communicator (pfaai_group_*);
+                                 6: pfaai_group_create_flags (PFAAI_GROUP_PEER_GATHER) */
 #define PFAAI_NTETRAMERS 160000 /* 20^4, interface.hpp:233 */
 
 /* Error codes: 0..3 have PFAAI_ERROR_CODE's values (interface.hpp:39-44). */
@@ -137,8 +138,11 @@ int pfaai_load(pfaai_ctx* ctx, const pfaai_problem* prob);
  * distributeGenomePairs, algorithm_impl.hpp:100-120).  The whole problem is
  * loaded; the per-entry walk data of all-vs-all rows (G_pos, G_end) is built
  * for those rows' genomes only, so a rank's load sorts and writes ~1/N of it.
- * Rows outside the block still run (through the run table: correct, slower).
- * Other modes: as pfaai_load. */
+ * Rows outside the block: when the caller hands over both F and G, the load
+ * checks G against F for the block's genomes only, so pfaai_run /
+ * pfaai_compute / pfaai_compute_rows / pfaai_stream refuse rows outside it
+ * (PFAAI_RC_INVALID); with G built on the device from F (or F from G) they
+ * run through the run table (correct, slower).  Other modes: as pfaai_load. */
 int pfaai_load_rows(pfaai_ctx* ctx, const pfaai_problem* prob, int64_t row_begin, int64_t row_end);
 
 /* F construction on the device (replaces DataStructHelper::constructLc /
@@ -251,9 +255,18 @@ int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint3
  * ncclRecv over xGMI; synchronous.  d_S / d_N are required with
  * PFAAI_FLAG_EMIT_JAC; PFAAI_FLAG_FULL_ROWS is not supported here.
  * Errors: PFAAI_RC_INVALID for a bad or repeated device id, PFAAI_RC_RCCL
- * for a communicator failure; pfaai_group_last_error gives the message. */
+ * for a communicator failure; pfaai_group_last_error gives the message.
+ * Row blocks: pfaai::split_rows with the first device's CU count, i.e. the
+ * cuts of bench.py's ranks (shard.split_rows(..., cus=)).
+ * pfaai_group_create_flags with PFAAI_GROUP_PEER_GATHER: no communicator;
+ * pfaai_group_run gathers each block by hipMemcpyPeerAsync on the first
+ * device's stream, after an event of the block's run, and a device id may
+ * repeat (several members on one GPU: the n > 1 path -- rank loads, block
+ * buffers, the gather's offsets -- on a one-GPU machine). */
+#define PFAAI_GROUP_PEER_GATHER 1u
 typedef struct pfaai_group pfaai_group;
 int pfaai_group_create(pfaai_group** group, const int* device_ids, int n_devices);
+int pfaai_group_create_flags(pfaai_group** group, const int* device_ids, int n_devices, uint32_t flags);
 int pfaai_group_destroy(pfaai_group* group);
 const char* pfaai_group_last_error(const pfaai_group* group);
 int pfaai_group_size(const pfaai_group* group, int* n_devices);

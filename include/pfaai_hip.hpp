@@ -93,8 +93,12 @@ void par_range(int64_t n, Fn fn) {
 // same cuts, pinned by tests/test_adapter_split.py): all-vs-all row a costs
 // fixed + width = 0.68 n + (n - 1 - a), times 0.93 for the narrow rows (width
 // <= 2047, the 512-thread launch); QT / QSUB rows are equal.  The prefix sums
-// are accumulated in row order in double, as numpy's cumsum does.
-inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
+// are accumulated in row order in double, as numpy's cumsum does.  cus > 0
+// (the device's compute units): the round-tail adjustment of shard.py's
+// split_rows(cus=...) -- a cut that leaves a block up to a quarter of a round
+// (2 * cus row workgroups) past a whole number of rounds, or up to that far
+// past the first narrow row, moves back to the boundary.
+inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all, int cus = 0) {
     std::vector<int64_t> cut{0};
     if (!all_vs_all) {
         for (int r = 1; r < parts; ++r) cut.push_back(n * r / parts);
@@ -116,7 +120,20 @@ inline std::vector<int64_t> split_rows(int64_t n, int parts, bool all_vs_all) {
         cut.push_back(std::min<int64_t>(std::max<int64_t>(i, cut.back()), n));
     }
     cut.push_back(n);
-    return cut;
+    if (cus <= 0 || parts <= 1) return cut;
+    const int64_t S = 2 * (int64_t)cus;  // shard.ROUND_TAIL = 0.25, NARROW_COLS = 2047
+    std::vector<int64_t> edge{0};
+    for (int k = 0; k + 1 < parts; ++k) {
+        const int64_t a = edge.back();
+        int64_t b = cut[(size_t)k + 1];
+        const int64_t m = b - a, tail = m % S;
+        if (m > S && 0 < tail && (double)tail <= 0.25 * (double)S && n - 1 - (b - 1) > 2047) b -= tail;
+        const int64_t narrow0 = n - 1 - 2047;
+        if (0 < b - narrow0 && (double)(b - narrow0) <= 0.25 * (double)S) b = narrow0;
+        edge.push_back(std::max(a, b));
+    }
+    edge.push_back(n);
+    return edge;
 }
 
 // Mode of a DSIT (see the header comment); specialise for other types.

@@ -39,11 +39,12 @@ EXPORTS = [
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
     "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_rows", "pfaai_load_timing", "pfaai_stream_matrix",
     "pfaai_load_info",
-    "pfaai_group_create", "pfaai_group_destroy", "pfaai_group_last_error", "pfaai_group_size", "pfaai_group_ctx",
-    "pfaai_group_load", "pfaai_group_blocks", "pfaai_group_run",
+    "pfaai_group_create", "pfaai_group_create_flags", "pfaai_group_destroy", "pfaai_group_last_error",
+    "pfaai_group_size", "pfaai_group_ctx", "pfaai_group_load", "pfaai_group_blocks", "pfaai_group_run",
 ]
+GROUP_PEER_GATHER = 1  # pfaai_group_create_flags
 LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
-ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist", 4: "v2"}
+ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist"}
 WALKS = {-1: "none", 0: "splitters", 3: "gpos"}  # pfaai_run_walk
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
@@ -120,6 +121,7 @@ def load_library(path=None):
         "pfaai_timing": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
         "pfaai_group_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+        "pfaai_group_create_flags": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int, u32]),
         "pfaai_group_destroy": (ctypes.c_int, [vp]),
         "pfaai_group_last_error": (ctypes.c_char_p, [vp]),
         "pfaai_group_size": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
@@ -374,13 +376,18 @@ class Group:
     """pfaai_group: several devices in one process, one RCCL communicator
     over them.  load() puts the problem on every device (each
     builds the walk data of its own row block); run() computes every block
-    and gathers them into device-0 arrays (grouped ncclSend / ncclRecv)."""
+    and gathers them into device-0 arrays (grouped ncclSend / ncclRecv).
+    peer_gather=True: no communicator, the gather by peer copies, and a
+    device may repeat (pfaai_group_create_flags, PFAAI_GROUP_PEER_GATHER)."""
 
-    def __init__(self, devices, lib_path=None):
+    def __init__(self, devices, lib_path=None, peer_gather=False):
         self.lib = load_library(lib_path)
         self.g = ctypes.c_void_p()
         ids = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
-        rc = self.lib.pfaai_group_create(ctypes.byref(self.g), ids, len(devices))
+        if peer_gather:
+            rc = self.lib.pfaai_group_create_flags(ctypes.byref(self.g), ids, len(devices), GROUP_PEER_GATHER)
+        else:
+            rc = self.lib.pfaai_group_create(ctypes.byref(self.g), ids, len(devices))
         if rc != PFAAI_OK:
             raise PfaaiError(rc, f"pfaai_group_create(devices={list(devices)})")
         self.n = len(devices)

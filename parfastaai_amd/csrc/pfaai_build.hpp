@@ -85,6 +85,18 @@ __global__ void k_fp16(const int32_t* __restrict__ Fp, int64_t n, uint16_t* __re
         Fp16[i] = (uint16_t)Fp[i];
 }
 
+// Member codes of F for k_rows_pl's WK 3 member scatter: genome b as
+// (b >> 1) << 7 | (b & 1) << 4, so that the counter word's LDS byte offset
+// is code >> 5 and the u16 half's increment is 1 << code (a VALU shift reads
+// the low 5 bits: 0 or 16) -- one VALU op per member fewer than from b.
+// n + 16 entries (the padding reads 0, like Fg's).
+__global__ void k_fcode(const int32_t* __restrict__ Fg, int64_t n, uint32_t* __restrict__ code) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + 16; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = i < n ? (uint32_t)Fg[i] : 0u;
+        code[i] = i < n ? ((b >> 1) << 7) | ((b & 1u) << 4) : 0u;
+    }
+}
+
 // Both F and G given: G must hold every membership of F, and an entry
 // (genome g, protein p, tetramer t) of G that is not in F is allowed only
 // where F has no run (t, p) at all (e.g. the -r path: G holds every tetramer

@@ -19,9 +19,6 @@
 #include "pfaai_hip.h"
 #include "pfaai_kernels.hpp"
 #include "pfaai_rows_pl.hpp"  // kernel constants (kPlEntries, kClkBlocks); templates only
-#ifdef PFAAI_DIAGNOSTICS
-#include "pfaai_rows_v2.hpp"  // k_rows_v2 (A/B only): built into libpfaai_hip_diag.so alone
-#endif
 
 // Diagnostic switches that change results or instrument the kernels
 // (PFAAI_ABLATE, PFAAI_BLK_ABLATE: skip kernel phases; PFAAI_PL_CLK: stage
@@ -66,6 +63,7 @@ struct pfaai_ctx {
     DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, G_pos, blk;
     DevBuf G_end;  // end of the F run of every G entry (with G_pos; k_rows_pl WK 3)
+    DevBuf Fcode;  // member codes of F (k_fcode; with G_end, the WK 3 member scatter)
     bool has_g = false;
     bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
     bool runs_key = false;
@@ -145,7 +143,7 @@ using namespace pfaai;
 constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
 constexpr int32_t kGposMaxIds = 20480;  // G_pos built for all-vs-all problems up to two row chunks wide
 
-enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3, RK_V2 = 4 };
+enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
 
 // scalars buffer layout (u64 each)
 // SC_HF / SC_HG: the both-given load's membership sums over F (k_hash_f) and
@@ -214,9 +212,6 @@ inline int pick_kw(int32_t max_cols, int kw_max) {
 // k_rows_pl's chunk width for this problem (launch_rows' KW choice)
 inline int64_t pl_chunk_cols(pfaai_ctx* c) {
     if (c->rows_kernel == RK_PL512) return 2 * 512 * (int64_t)pick_kw<512>(c->cols_run, 10);
-#ifdef PFAAI_DIAGNOSTICS
-    if (c->rows_kernel == RK_V2) return 2 * (int64_t)kV2Threads * pick_kw<kV2Threads>(c->cols_run, 5);
-#endif
     const char* km = DIAG_ENV("PFAAI_PL_KWMAX");
     return 2 * 1024 * (int64_t)pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 }

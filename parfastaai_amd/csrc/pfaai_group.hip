@@ -14,11 +14,16 @@
 //         stream) into a block buffer; the blocks are gathered into the
 //         caller's device-0 arrays by grouped ncclSend / ncclRecv over xGMI
 //         (ncclGather needs equal counts; the blocks are not) -- device 0
-//         writes its own block in place.
-// Row blocks: pfaai::split_rows (the row-cost model of shard.py, the cuts
-// bench.py's ranks use).  ALL and QT rows map to disjoint contiguous JAC
-// spans; QSUB rows do not (each row has two segments), so a QSUB problem
-// runs on device 0 alone.
+//         writes its own block in place.  PFAAI_GROUP_PEER_GATHER: no
+//         communicator; each block is copied by hipMemcpyPeerAsync on
+//         device 0's stream after an event of its device's run, and a device
+//         may appear more than once -- so one GPU hosts an n-member group and
+//         runs every piece of the n > 1 path but the RCCL calls
+//         (tests/test_gpu_group.py).
+// Row blocks: pfaai::split_rows with the first device's CU count (the
+// row-cost model and round-tail cuts of shard.py, the cuts bench.py's ranks
+// use).  ALL and QT rows map to disjoint contiguous JAC spans; QSUB rows do
+// not (each row has two segments), so a QSUB problem runs on device 0 alone.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
@@ -39,6 +44,8 @@ struct pfaai_group {
     std::vector<pfaai_ctx*> ctx;
     std::vector<ncclComm_t> comm;
     std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> done;       // PEER_GATHER: a device's block is computed
+    uint32_t flags = 0;
     std::vector<int64_t> cut;           // row blocks [cut[i], cut[i+1])
     std::vector<int64_t> first, count;  // their JAC spans
     std::vector<void*> blk[3];          // devices 1..n-1: block buffers of AJI, S, N
@@ -104,11 +111,26 @@ int ctx_fail(pfaai_group* g, int i, int rc) {
         if (e_ != hipSuccess) return gfail(g, PFAAI_RC_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-#define GNCCL(g, expr)                                                                             \
+// inside an ncclGroupStart / ncclGroupEnd bracket: a failed call closes the
+// bracket (a group left open defers or hangs this thread's later RCCL calls)
+#define GNCCL_IN_GROUP(g, expr)                                                                    \
     do {                                                                                           \
         const ncclResult_t r_ = (expr);                                                            \
-        if (r_ != ncclSuccess) return gfail(g, PFAAI_RC_RCCL, std::string(#expr) + ": " + rccl().GetErrorString(r_)); \
+        if (r_ != ncclSuccess) {                                                                   \
+            (void)rccl().GroupEnd();                                                               \
+            return gfail(g, PFAAI_RC_RCCL, std::string(#expr) + ": " + rccl().GetErrorString(r_)); \
+        }                                                                                          \
     } while (0)
+
+// wait for the blocks already launched (devices < upto) before an error
+// return: their kernels write the caller's or the group's buffers
+void drain(pfaai_group* g, int upto) {
+    for (int i = 0; i < upto && i < g->n; ++i)
+        if (g->st[i]) {
+            (void)hipSetDevice(g->dev[i]);
+            (void)hipStreamSynchronize(g->st[i]);
+        }
+}
 
 void release_blocks(pfaai_group* g) {
     for (int k = 0; k < 3; ++k) {
@@ -143,23 +165,26 @@ int ensure_block(pfaai_group* g, int k, int i) {
 
 extern "C" {
 
-int pfaai_group_create(pfaai_group** out, const int* device_ids, int n_devices) {
+int pfaai_group_create_flags(pfaai_group** out, const int* device_ids, int n_devices, uint32_t flags) {
     if (!out) return PFAAI_RC_INVALID;
     *out = nullptr;
-    if (!device_ids || n_devices < 1) return PFAAI_RC_INVALID;
+    if (!device_ids || n_devices < 1 || (flags & ~(uint32_t)PFAAI_GROUP_PEER_GATHER)) return PFAAI_RC_INVALID;
+    const bool peer = flags & PFAAI_GROUP_PEER_GATHER;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) return PFAAI_RC_HIP;
     for (int i = 0; i < n_devices; ++i) {
         if (device_ids[i] < 0 || device_ids[i] >= ndev) return PFAAI_RC_INVALID;
-        for (int j = 0; j < i; ++j)
-            if (device_ids[j] == device_ids[i]) return PFAAI_RC_INVALID;  // (one rank per device)
+        for (int j = 0; j < i && !peer; ++j)
+            if (device_ids[j] == device_ids[i]) return PFAAI_RC_INVALID;  // (one RCCL rank per device)
     }
     auto* g = new (std::nothrow) pfaai_group;
     if (!g) return PFAAI_RC_OOM;
     g->n = n_devices;
+    g->flags = flags;
     g->dev.assign(device_ids, device_ids + n_devices);
     g->ctx.assign(n_devices, nullptr);
     g->st.assign(n_devices, nullptr);
+    g->done.assign(n_devices, nullptr);
     g->comm.assign(n_devices, nullptr);
     release_blocks(g);
     int rc = PFAAI_RC_OK;
@@ -167,8 +192,18 @@ int pfaai_group_create(pfaai_group** out, const int* device_ids, int n_devices) 
         rc = pfaai_create(&g->ctx[i], g->dev[i]);
         if (rc == PFAAI_RC_OK) {
             (void)hipSetDevice(g->dev[i]);
-            if (hipStreamCreateWithFlags(&g->st[i], hipStreamNonBlocking) != hipSuccess) rc = PFAAI_RC_HIP;
+            if (hipStreamCreateWithFlags(&g->st[i], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess)
+                rc = PFAAI_RC_HIP;
         }
+    }
+    if (peer) {
+        if (rc != PFAAI_RC_OK) {
+            pfaai_group_destroy(g);
+            return rc;
+        }
+        *out = g;
+        return PFAAI_RC_OK;
     }
     if (rc == PFAAI_RC_OK && !rccl().ok) {
         g->err = "librccl.so.1 not found (or lacks a symbol)";
@@ -186,6 +221,10 @@ int pfaai_group_create(pfaai_group** out, const int* device_ids, int n_devices) 
     return PFAAI_RC_OK;
 }
 
+int pfaai_group_create(pfaai_group** out, const int* device_ids, int n_devices) {
+    return pfaai_group_create_flags(out, device_ids, n_devices, 0u);
+}
+
 int pfaai_group_destroy(pfaai_group* g) {
     if (!g) return PFAAI_RC_OK;
     for (int i = 0; i < g->n; ++i)
@@ -200,6 +239,10 @@ int pfaai_group_destroy(pfaai_group* g) {
         if (g->st[i]) {
             (void)hipSetDevice(g->dev[i]);
             (void)hipStreamDestroy(g->st[i]);
+        }
+        if (g->done[i]) {
+            (void)hipSetDevice(g->dev[i]);
+            (void)hipEventDestroy(g->done[i]);
         }
         if (g->ctx[i]) pfaai_destroy(g->ctx[i]);
     }
@@ -228,7 +271,9 @@ int pfaai_group_load(pfaai_group* g, const pfaai_problem* prob) {
         g->cut.assign(n + 1, rows);
         g->cut[0] = 0;
     } else {
-        g->cut = pfaai::split_rows(rows, n, prob->mode == PFAAI_MODE_ALL);
+        int cus = 0;  // the round-tail cuts of bench.py's ranks (shard.split_rows(cus=...))
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, g->dev[0]) != hipSuccess) cus = 0;
+        g->cut = pfaai::split_rows(rows, n, prob->mode == PFAAI_MODE_ALL, cus);
     }
     // concurrent loads, one host thread per device context
     std::vector<int> rc(n, PFAAI_RC_OK);
@@ -282,29 +327,55 @@ int pfaai_group_run(pfaai_group* g, uint32_t flags, double* d_aji, double* d_S, 
             if (i == 0) {
                 base[k] = out[k];
             } else {
-                if ((r = ensure_block(g, k, i))) return r;
+                if ((r = ensure_block(g, k, i))) {
+                    drain(g, i);
+                    return r;
+                }
                 base[k] = static_cast<char*>(g->blk[k][i]) - (ptrdiff_t)(g->first[i] * (int64_t)esz[k]);
             }
         }
         if ((r = pfaai_run(g->ctx[i], g->cut[i], g->cut[i + 1], flags, static_cast<double*>(base[0]),
-                           static_cast<double*>(base[1]), static_cast<int32_t*>(base[2]), g->st[i])))
+                           static_cast<double*>(base[1]), static_cast<int32_t*>(base[2]), g->st[i]))) {
+            drain(g, g->n);
             return ctx_fail(g, i, r);
+        }
     }
-    // the gather into device 0's arrays: grouped point-to-point transfers
-    if (g->n > 1) {
+    if (g->n > 1 && (g->flags & PFAAI_GROUP_PEER_GATHER)) {
+        // the gather by peer copies on device 0's stream, each after its block
+        for (int i = 1; i < g->n; ++i) {
+            if (g->count[i] <= 0) continue;
+            GHIP(g, hipSetDevice(g->dev[i]));
+            GHIP(g, hipEventRecord(g->done[i], g->st[i]));
+            GHIP(g, hipSetDevice(g->dev[0]));
+            GHIP(g, hipStreamWaitEvent(g->st[0], g->done[i], 0));
+            for (int k = 0; k < 3; ++k) {
+                if (!out[k]) continue;
+                GHIP(g, hipMemcpyPeerAsync(static_cast<char*>(out[k]) + g->first[i] * (int64_t)esz[k], g->dev[0],
+                                           g->blk[k][i], g->dev[i], (size_t)g->count[i] * esz[k], g->st[0]));
+            }
+        }
+    } else if (g->n > 1) {
+        // the gather into device 0's arrays: grouped point-to-point transfers
         const Rccl& R = rccl();
-        GNCCL(g, R.GroupStart());
+        if (R.GroupStart() != ncclSuccess) {
+            drain(g, g->n);
+            return gfail(g, PFAAI_RC_RCCL, "ncclGroupStart failed");
+        }
         for (int i = 1; i < g->n; ++i) {
             if (g->count[i] <= 0) continue;
             for (int k = 0; k < 3; ++k) {
                 if (!out[k]) continue;
                 const ncclDataType_t t = k == 2 ? ncclInt32 : ncclFloat64;
-                GNCCL(g, R.Send(g->blk[k][i], (size_t)g->count[i], t, 0, g->comm[i], g->st[i]));
-                GNCCL(g, R.Recv(static_cast<char*>(out[k]) + g->first[i] * (int64_t)esz[k], (size_t)g->count[i], t, i,
-                                g->comm[0], g->st[0]));
+                GNCCL_IN_GROUP(g, R.Send(g->blk[k][i], (size_t)g->count[i], t, 0, g->comm[i], g->st[i]));
+                GNCCL_IN_GROUP(g, R.Recv(static_cast<char*>(out[k]) + g->first[i] * (int64_t)esz[k], (size_t)g->count[i], t,
+                                         i, g->comm[0], g->st[0]));
             }
         }
-        GNCCL(g, R.GroupEnd());
+        const ncclResult_t re = R.GroupEnd();
+        if (re != ncclSuccess) {
+            drain(g, g->n);
+            return gfail(g, PFAAI_RC_RCCL, std::string("ncclGroupEnd: ") + R.GetErrorString(re));
+        }
     }
     for (int i = 0; i < g->n; ++i) {
         GHIP(g, hipSetDevice(g->dev[i]));

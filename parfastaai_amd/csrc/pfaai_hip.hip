@@ -278,7 +278,7 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     const int64_t wcols = pl_chunk_cols(c);
     {
         const char* wv = DIAG_ENV("PFAAI_PL_WINDOWS");
-        c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512 || c->rows_kernel == RK_V2) &&
+        c->windows = (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) &&
                      !(wv && wv[0] == '0') &&
                      (int64_t)c->cols_run + 1 > wcols;
         if (c->windows) {  // all windows' tables staged in one k_blk workgroup's LDS (nwin * P <= 5104)
@@ -1314,6 +1314,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
                 HIPCHK(c, hipGetLastError());
             }
         }
+        // member codes for the WK 3 walks (all-vs-all with G_pos / G_end)
+        d.Fcode = nullptr;
+        if (d.G_end && p.mode == PFAAI_MODE_ALL) {
+            if ((rc = ensure(c, c->Fcode, (size_t)(n_f + 16) * sizeof(uint32_t)))) return rc;
+            hipLaunchKernelGGL(k_fcode, dim3((int)std::min<int64_t>(ceil_div(n_f + 16, 256), 1 << 16)), dim3(256), 0, s,
+                               d.Fg, n_f, static_cast<uint32_t*>(c->Fcode.p));
+            HIPCHK(c, hipGetLastError());
+            d.Fcode = static_cast<const uint32_t*>(c->Fcode.p);
+        } else {
+            release(c->Fcode);
+        }
         if (g_check && (rc = finish_g_check(c, s))) {
             if (rc == -1)
                 return fail(c, PFAAI_RC_INVALID,
@@ -1414,7 +1425,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->Fcode, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw, &c->srec_a, &c->srec_b, &c->shist,
                       &c->sgsum, &c->sbase, &c->tails, &c->ranks})
@@ -1498,18 +1509,15 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         if (const char* v = DIAG_ENV("PFAAI_ROWS_KERNEL")) {
             const std::string x(v);
             if (x == "pl") k = RK_PL;
-#ifdef PFAAI_DIAGNOSTICS
-            else if (x == "v2") k = RK_V2;
-#endif
             else if (x == "pl512") k = RK_PL512;
             else if (x == "fused") k = RK_FUSED;
             else if (x == "worklist") k = RK_WORKLIST;
-            else return fail(c, PFAAI_RC_INVALID, "PFAAI_ROWS_KERNEL must be pl, v2, pl512, fused or worklist");
+            else return fail(c, PFAAI_RC_INVALID, "PFAAI_ROWS_KERNEL must be pl, pl512, fused or worklist");
         }
         if (!c->has_g && k != RK_WORKLIST) k = RK_WORKLIST;       // the others walk the G lists
         if (c->max_glen > kPlEntries && k != RK_WORKLIST) k = RK_FUSED;  // lists too long
         // k_rows_pl addresses the run table with 32-bit buffer offsets
-        if ((uint64_t)c->prob.n_prot * PFAAI_NTETRAMERS * 16u >= (1ull << 32) && (k == RK_PL || k == RK_PL512 || k == RK_V2))
+        if ((uint64_t)c->prob.n_prot * PFAAI_NTETRAMERS * 16u >= (1ull << 32) && (k == RK_PL || k == RK_PL512))
             k = RK_FUSED;
         c->rows_kernel = k;
     }

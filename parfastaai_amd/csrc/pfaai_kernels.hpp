@@ -62,6 +62,7 @@ struct Dev {
     const int32_t* G_tet;
     const uint32_t* G_pos;      // [|G|] F index of each G entry (all-vs-all; nullptr if not built)
     const uint32_t* G_end;      // [|G|] end of the F run of each G entry (built with G_pos)
+    const uint32_t* Fcode;      // [|F| + 16] member codes of F for the WK 3 walks (k_fcode), or nullptr
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
     const uint16_t* Fp16;       // [|F|] protein of each F entry, u16 (k_blk)
     const uint16_t* T16;        // [n_prot][t16_cols] T by column genome id, u16 (k_rows_pl)

@@ -1,37 +1,29 @@
-// pfaai_launch.hpp -- launchers of the row kernels (k_rows_pl, k_rows_v2,
-// k_rows): kernel variant, counter words per thread, column chunks and
-// column windows.  Included by the per-mode translation units
-// pfaai_rows_m{0,1,2}.hip only.
+// pfaai_launch.hpp -- launchers of the row kernels (k_rows_pl, k_rows):
+// kernel variant, counter words per thread, column chunks and column
+// windows.  Included by the per-mode translation units pfaai_rows_m{0..3}.hip
+// only.
 #pragma once
 #include "pfaai_ctx.hpp"
 #include "pfaai_rows_pl.hpp"
-#ifdef PFAAI_DIAGNOSTICS
-#include "pfaai_rows_v2.hpp"
-#endif
 
 namespace pfaai_impl {
 
-// k_rows_pl's lookahead form (LA): measured no faster on the narrow
-// launches it fits (8-way shards at 10k: last shard 1.08 -> 1.10 ms, stage
-// clocks in profiles/r03n_*: the per-protein chain of a narrow row is the
-// busy waves' instruction stream, not the member-load latency LA hides), so
-// the product does not take it; the diagnostics build keeps it for A/B
-// (PFAAI_PL_LAKW=<max KW>, PFAAI_PL_CLK_LA=1 for its stage clocks)
-constexpr int kLaKwMax = 0;
-#ifdef PFAAI_DIAGNOSTICS
-constexpr int kLaKwInst = 5;  // (KW 4 / 5 spill)
-#else
-constexpr int kLaKwInst = 0;
-#endif
+// k_rows_pl's variant bits for the WK 3 walks (pfaai_rows_pl.hpp V): the
+// release forms kPlV (1024 threads) and 0 (the 512-thread narrow rows);
+// PFAAI_PL_V=0..3 overrides both (diagnostics, A/B).
+constexpr int kPlV = 3;
+template <int NT>
+inline int pl_v() {
+    const char* v = DIAG_ENV("PFAAI_PL_V");
+    return v ? std::max(0, std::min(3, atoi(v))) : NT == 1024 ? kPlV : 0;
+}
 
-template <int MODE, int KW, int NT, int WPE = 4, int NK = 0, bool BR = true, int VAR = 0>
+template <int MODE, int KW, int NT, int WPE, int NK>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                hipStream_t s) {
     const int32_t chunk = 2 * KW * NT;
     const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-    const size_t nbytes = NK != 1 ? 0 : (VAR & 1024) ? (size_t)KW * NT * 2 : (size_t)(KW + 1) / 2 * NT * 4;  // N (u8)
-    const size_t lds = (2 * (size_t)KW * NT + c->prob.n_prot + 1) * sizeof(uint32_t) + nbytes +
-                       (((size_t)c->prob.n_prot + 1) / 2) * sizeof(uint32_t);  // + T[p][A] (u16)
+    const size_t lds = pl_lds_bytes<KW, NT, NK>(c->prob.n_prot);
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     // |F| past 2^30 entries: member loads by 64-bit address (PFAAI_PL_BIGF=1 forces it, A/B)
     const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || DIAG_ENV("PFAAI_PL_BIGF");
@@ -42,48 +34,30 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     // all-vs-all rows in one chunk with G_pos loaded: each run walk starts just
     // past the row genome (k_rows_pl WK 3, pl_issue_m2<A8>)
     const bool gp = MODE == 0 && wk == 1 && pl_uses_ends(c, MODE);
-    // the lookahead form (member loads one protein ahead, k_rows_pl LA) where
-    // its registers fit: KW <= kLaKwMax (PFAAI_PL_LAKW=0..5 in diagnostics, A/B)
-    int la_kw = kLaKwMax;
-    if (const char* v = DIAG_ENV("PFAAI_PL_LAKW")) la_kw = atoi(v);
-    const bool la = gp && NK == 1 && NT == 1024 && KW <= la_kw;
     auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
-#define PLK(BF, WKV)                                                                                                 \
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, WKV>), dim3(r1 - r0, gy), dim3(NT), lds, \
-                       s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
-#define PLKA(BF)                                                                                                     \
-    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, true, BR, VAR, 3, true>), dim3(r1 - r0, gy), dim3(NT), \
-                       lds, s, dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+#define PLK(BF, WKV, VV)                                                                                             \
+    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, WKV, VV>), dim3(r1 - r0, gy), dim3(NT), lds, s, \
+                       dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
         c->last_walk = gp ? PFAAI_WALK_GPOS : PFAAI_WALK_SPLITTERS;
         if (wk == 0 || abs_chunk >= 0) {
             c->last_walk = PFAAI_WALK_SPLITTERS;
-            if (bigf) PLK(true, 0); else PLK(false, 0);
+            if (bigf) PLK(true, 0, 0); else PLK(false, 0, 0);
         } else if constexpr (kWk1 != 0) {
             if constexpr (MODE == 0) {
-                if constexpr (NK == 1 && NT == 1024 && KW <= kLaKwInst) {
-                    if (la) {
-#ifdef PFAAI_DIAGNOSTICS
-                        if (!bigf && DIAG_ENV("PFAAI_PL_CLK_LA") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {  // stage clocks (the G_pos path stays on: not PFAAI_PL_CLK)
-                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, true, BR, VAR, 3, true>),
-                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, abs_chunk, flags,
-                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
-                                               static_cast<unsigned long long*>(c->dbg.p));
-                            return;
-                        }
-#endif
-                        if (bigf) PLKA(true); else PLKA(false);
-                        return;
+                if (gp) {  // (G_pos is built up to 20 480 genomes only: never BIGF)
+                    if (bigf) { PLK(true, 3, 0); return; }
+                    switch (pl_v<NT>()) {
+                        case 1: PLK(false, 3, 1); break;
+                        case 2: PLK(false, 3, 2); break;
+                        case 3: PLK(false, 3, 3); break;
+                        default: PLK(false, 3, 0); break;
                     }
-                }
-                if (gp) {
-                    if (bigf) PLK(true, 3); else PLK(false, 3);
                     return;
                 }
             }
-            if (bigf) PLK(true, kWk1); else PLK(false, kWk1);
+            if (bigf) PLK(true, kWk1, 0); else PLK(false, kWk1, 0);
         }
 #undef PLK
-#undef PLKA
     };
     if (nchunks == 1 || !c->windows) {
         rows(c->dev, rb, re, nchunks, -1);
@@ -104,50 +78,14 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     }
 }
 
-#ifdef PFAAI_DIAGNOSTICS
-// k_rows_v2 (pfaai_rows_v2.hpp): one 1024-thread workgroup per CU, same
-// chunk and column-window rules as launch_pl
-template <int MODE, int KW>
-void launch_v2(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
-               hipStream_t s) {
-    const int32_t chunk = 2 * KW * kV2Threads;
-    const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-    const size_t lds = (4 * (size_t)KW * kV2Threads + c->prob.n_prot + 1) * sizeof(uint32_t);  // u32 counters x 2
-    auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-    const bool bigf = (uint64_t)(c->prob.n_f + 16) * 4u > 0xFFFFFFFFull || DIAG_ENV("PFAAI_PL_BIGF");
-    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
-#ifdef PFAAI_DIAGNOSTICS
-        if (KW == 5 && !bigf && DIAG_ENV("PFAAI_V2_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
-            hipLaunchKernelGGL((k_rows_v2<MODE, KW, false, true>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0,
-                               chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
-                               static_cast<unsigned long long*>(c->dbg.p));
-            return;
-        }
-#endif
-        if (bigf)
-            hipLaunchKernelGGL((k_rows_v2<MODE, KW, true>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0, chunk,
-                               abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-        else
-            hipLaunchKernelGGL((k_rows_v2<MODE, KW, false>), dim3(r1 - r0, gy), dim3(kV2Threads), lds, s, dv, r0,
-                               chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS);
-    };
-    if (nchunks == 1 || !c->windows) {
-        rows(c->dev, rb, re, nchunks, -1);
-        return;
-    }
-    const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
-    const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
-    for (int32_t w = 0; w < nwin; ++w) {
-        int64_t r1 = re;
-        if (MODE == 0) r1 = std::min<int64_t>(re, (int64_t)(w + 1) * chunk - 1);  // row a has columns a+1 ..
-        if (r1 <= rb) continue;
-        Dev dw = c->dev;
-        dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
-        rows(dw, rb, r1, 1, w);
-    }
+// One k_rows_pl launch shape (KW, NT, WPE) with the N storage (nl: u8 in
+// LDS, P <= 255; else u16 in registers).
+template <int MODE, int KW, int NT, int WPE>
+void launch_pl_n(pfaai_ctx* c, bool nl, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S,
+                   int32_t* N, hipStream_t s) {
+    if (nl) launch_pl<MODE, KW, NT, WPE, 1>(c, rb, re, flags, aji, S, N, s);
+    else launch_pl<MODE, KW, NT, WPE, 0>(c, rb, re, flags, aji, S, N, s);
 }
-
-#endif
 
 template <int MODE, int KW>
 void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
@@ -192,9 +130,9 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
         c->last_narrow = true;
         c->cols_run = (int32_t)(n - 1 - cut);  // the narrow launch's widest row
         if (pick_kw<512>(c->cols_run, 2) == 1)
-            launch_pl<0, 1, 512, 8, 1, true>(c, cut, re, flags, aji, S, N, st);
+            launch_pl_n<0, 1, 512, 8>(c, true, cut, re, flags, aji, S, N, st);
         else
-            launch_pl<0, 2, 512, 8, 1, true>(c, cut, re, flags, aji, S, N, st);
+            launch_pl_n<0, 2, 512, 8>(c, true, cut, re, flags, aji, S, N, st);
         c->cols_run = cols_all;
     };
     if (cut == rb) {
@@ -207,11 +145,11 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
         return false;
     narrow(c->side_stream);
     switch (pick_kw<1024>(cols_all, 5)) {
-        case 1: launch_pl<0, 1, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
-        case 2: launch_pl<0, 2, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
-        case 3: launch_pl<0, 3, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
-        case 4: launch_pl<0, 4, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
-        default: launch_pl<0, 5, 1024, 8, 1, true>(c, rb, cut, flags, aji, S, N, s); break;
+        case 1: launch_pl_n<0, 1, 1024, 8>(c, true, rb, cut, flags, aji, S, N, s); break;
+        case 2: launch_pl_n<0, 2, 1024, 8>(c, true, rb, cut, flags, aji, S, N, s); break;
+        case 3: launch_pl_n<0, 3, 1024, 8>(c, true, rb, cut, flags, aji, S, N, s); break;
+        case 4: launch_pl_n<0, 4, 1024, 8>(c, true, rb, cut, flags, aji, S, N, s); break;
+        default: launch_pl_n<0, 5, 1024, 8>(c, true, rb, cut, flags, aji, S, N, s); break;
     }
     (void)hipEventRecord(c->narrow_ev[1], c->side_stream);
     (void)hipStreamWaitEvent(s, c->narrow_ev[1], 0);
@@ -221,42 +159,26 @@ inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, 
 template <int MODE>
 void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                  hipStream_t s) {
-#define PL_CASE(NT, K) \
-    case K: launch_pl<MODE, K, NT>(c, rb, re, flags, aji, S, N, s); break;
 #define KR_CASE(K) \
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
+    // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
+    const bool nl = c->prob.n_prot <= 255 && !DIAG_ENV("PFAAI_PL_NREG");
     if constexpr (MODE != kModeFull) {  // full rows: k_rows_pl / fused only
-#ifdef PFAAI_DIAGNOSTICS
-        if (c->rows_kernel == RK_V2) {
-            switch (pick_kw<kV2Threads>(c->cols_run, 5)) {
-                case 1: launch_v2<MODE, 1>(c, rb, re, flags, aji, S, N, s); break;
-                case 2: launch_v2<MODE, 2>(c, rb, re, flags, aji, S, N, s); break;
-                case 3: launch_v2<MODE, 3>(c, rb, re, flags, aji, S, N, s); break;
-                case 4: launch_v2<MODE, 4>(c, rb, re, flags, aji, S, N, s); break;
-                default: launch_v2<MODE, 5>(c, rb, re, flags, aji, S, N, s); break;
-            }
-            return;
-        }
-#endif
         if (c->rows_kernel == RK_PL512) {
-            // 512-thread workgroups, four per CU (<= 64 VGPRs) with N in LDS
-            // where P <= 255 -- and the WK 3 walks (pl_uses_ends) -- for A/B
-            // of narrow launches (more rows in flight per CU)
-            if (c->prob.n_prot <= 255) {
-                switch (pick_kw<512>(c->cols_run, 10)) {
-                    case 1: launch_pl<MODE, 1, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                    case 2: launch_pl<MODE, 2, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                    case 3: launch_pl<MODE, 3, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                    case 4: launch_pl<MODE, 4, 512, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                    PL_CASE(512, 5) PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
-                    default: break;
-                }
-                return;
-            }
+            // 512-thread workgroups, four per CU (<= 64 VGPRs), for A/B of
+            // narrow launches (more rows in flight per CU); KW >= 5 keeps N
+            // in registers at two workgroups per CU
             switch (pick_kw<512>(c->cols_run, 10)) {
-                PL_CASE(512, 1) PL_CASE(512, 2) PL_CASE(512, 3) PL_CASE(512, 4) PL_CASE(512, 5)
-                PL_CASE(512, 6) PL_CASE(512, 7) PL_CASE(512, 8) PL_CASE(512, 9) PL_CASE(512, 10)
-                default: break;
+                case 1: launch_pl_n<MODE, 1, 512, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+                case 2: launch_pl_n<MODE, 2, 512, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+                case 3: launch_pl_n<MODE, 3, 512, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+                case 4: launch_pl_n<MODE, 4, 512, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+                case 5: launch_pl_n<MODE, 5, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
+                case 6: launch_pl_n<MODE, 6, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
+                case 7: launch_pl_n<MODE, 7, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
+                case 8: launch_pl_n<MODE, 8, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
+                case 9: launch_pl_n<MODE, 9, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
+                default: launch_pl_n<MODE, 10, 512, 4>(c, false, rb, re, flags, aji, S, N, s); break;
             }
             return;
         }
@@ -265,62 +187,28 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         const char* km = DIAG_ENV("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);
 #ifdef PFAAI_DIAGNOSTICS
+        // stage clocks at the benchmark shape (PFAAI_PL_CLK, tools/gpu/stage_clocks.py)
         if (MODE == 0 && kw == 5 && !c->windows && c->prob.n_prot <= 255 && DIAG_ENV("PFAAI_PL_CLK") &&
             c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
-            const int32_t chunk = 2 * 5 * 1024;  // diagnostics: stage clocks at the benchmark shape
+            const int32_t chunk = 2 * 5 * 1024;
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
-            const size_t lds = (2 * (size_t)5 * 1024 + c->prob.n_prot + 1) * sizeof(uint32_t) + 3 * 1024 * 4 +
-                               (((size_t)c->prob.n_prot + 1) / 2) * sizeof(uint32_t);
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
-            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, true, true>), dim3(re - rb, nchunks), dim3(1024), lds, s, c->dev, rb,
-                               chunk, -1, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS,
-                               static_cast<unsigned long long*>(c->dbg.p));
+            auto* clk = static_cast<unsigned long long*>(c->dbg.p);
+            hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, 1, 0>), dim3(re - rb, nchunks), dim3(1024),
+                               (pl_lds_bytes<5, 1024, 1>(c->prob.n_prot)), s, c->dev, rb, chunk, -1, flags,
+                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
             return;
         }
 #endif
-#ifdef PFAAI_DIAGNOSTICS
-        // A/B of the N storage (NK) and S5 form (BR) at the benchmark shape
-        if (const char* v = DIAG_ENV("PFAAI_PL_VAR"); v && MODE == 0 && kw == 5 && c->prob.n_prot <= 255) {
-            const std::string sv(v);
-            if (sv == "nk0br") { launch_pl<MODE, 5, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk1br") { launch_pl<MODE, 5, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk2br") { launch_pl<MODE, 5, 1024, 8, 2, true>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk0") { launch_pl<MODE, 5, 1024, 8, 0, false>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk1") { launch_pl<MODE, 5, 1024, 8, 1, false>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk2") { launch_pl<MODE, 5, 1024, 8, 2, false>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "ABLATE_nodiv") { launch_pl<MODE, 5, 1024, 8, 1, true, 1>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk1br_v2") { launch_pl<MODE, 5, 1024, 8, 1, true, 2>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk1br_v4") { launch_pl<MODE, 5, 1024, 8, 1, true, 4>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "nk1br_v6") { launch_pl<MODE, 5, 1024, 8, 1, true, 6>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "tearly") { launch_pl<MODE, 5, 1024, 8, 1, true, 32>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "g4") { launch_pl<MODE, 5, 1024, 8, 1, true, 8>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "noskip") { launch_pl<MODE, 5, 1024, 8, 1, true, 64>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "n16") { launch_pl<MODE, 5, 1024, 8, 1, true, 1024>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "s1skip") { launch_pl<MODE, 5, 1024, 8, 1, true, 128>(c, rb, re, flags, aji, S, N, s); return; }
-            if (sv == "bf") { launch_pl<MODE, 5, 1024, 8, 1, true, 256>(c, rb, re, flags, aji, S, N, s); return; }
-        }
-#endif
-        // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
-        const bool nl = c->prob.n_prot <= 255 && !DIAG_ENV("PFAAI_PL_NREG");
         if constexpr (MODE == 0) {
             if (nl && launch_narrow(c, rb, re, flags, aji, S, N, s)) return;
         }
-        if (nl) {
-            switch (kw) {
-                case 1: launch_pl<MODE, 1, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 2: launch_pl<MODE, 2, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 3: launch_pl<MODE, 3, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                case 4: launch_pl<MODE, 4, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-                default: launch_pl<MODE, 5, 1024, 8, 1, true>(c, rb, re, flags, aji, S, N, s); break;
-            }
-            return;
-        }
         switch (kw) {
-            case 1: launch_pl<MODE, 1, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
-            case 2: launch_pl<MODE, 2, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
-            case 3: launch_pl<MODE, 3, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
-            case 4: launch_pl<MODE, 4, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
-            default: launch_pl<MODE, 5, 1024, 8, 0, true>(c, rb, re, flags, aji, S, N, s); break;
+            case 1: launch_pl_n<MODE, 1, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+            case 2: launch_pl_n<MODE, 2, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+            case 3: launch_pl_n<MODE, 3, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+            case 4: launch_pl_n<MODE, 4, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
+            default: launch_pl_n<MODE, 5, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;
         }
     } else {
         switch (pick_kw<kRowThreads>(c->cols_run, 10)) {
@@ -330,7 +218,6 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             default: break;
         }
     }
-#undef PL_CASE
 #undef KR_CASE
 }
 
@@ -340,7 +227,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
 template <int MODE>
 void preload_rows() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_rows_pl<MODE, 5, 1024, 8, false, 1, false, true, true, 0, 0>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_rows_pl<MODE, 5, 1024, 8, false, 1, false, 0, 0>));
 }
 
 }  // namespace pfaai_impl

@@ -28,7 +28,7 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert _capi.load_library().pfaai_version() == 5
+    assert _capi.load_library().pfaai_version() == 6
 
 
 def test_problem_struct_layout():
@@ -67,15 +67,15 @@ def test_product_does_not_import_oracle():
 
 AB_SWITCHES = (b"PFAAI_ROWS_KERNEL", b"PFAAI_XCD_CHUNK", b"PFAAI_PL_PRIO", b"PFAAI_PL_LAUNCH_COLS",
                b"PFAAI_PL_WINDOWS", b"PFAAI_BLK_THREADS", b"PFAAI_BLK_QT_SPLIT", b"PFAAI_BLK_END_TILE",
-               b"PFAAI_BLK_END_U", b"PFAAI_PL_KWMAX", b"PFAAI_PL_BIGF", b"PFAAI_PL_NREG")
+               b"PFAAI_BLK_END_U", b"PFAAI_PL_KWMAX", b"PFAAI_PL_BIGF", b"PFAAI_PL_NREG", b"PFAAI_PL_V")
 
 
 def test_release_library_ignores_diagnostic_switches():
     """The result-changing ablations, the stage-clock instrumentation and
     every A/B kernel switch exist only in libpfaai_hip_diag.so
     (-DPFAAI_DIAGNOSTICS): the release library does not even contain their
-    names, so no environment can change its kernel choice or results; the
-    rejected k_rows_v2 is compiled into the diagnostics build alone."""
+    names, so no environment can change its kernel choice or results.  The
+    rejected k_rows_v2 of rounds 2-4 is compiled into neither."""
     blob = open(_capi.LIB_PATH, "rb").read()
     for name in (b"PFAAI_ABLATE", b"PFAAI_BLK_ABLATE", b"PFAAI_PL_CLK", b"PFAAI_DIV_NEWTON") + AB_SWITCHES:
         assert name not in blob, name
@@ -83,4 +83,4 @@ def test_release_library_ignores_diagnostic_switches():
     diag = open(_capi.DIAG_LIB_PATH, "rb").read()
     for name in AB_SWITCHES:
         assert name in diag, name
-    assert b"k_rows_v2" in diag
+    assert b"k_rows_v2" not in diag

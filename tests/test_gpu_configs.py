@@ -7,9 +7,13 @@ them: |E| > 2^31, ds_helper.hpp:209,365; N >= 46 342, ds_impl.hpp:79).
       the whole S / N / AJI vectors equal the oracle's (SHA-256 digests).
   C3  SYN 10 000 x 100 all-vs-all: the whole S / N / AJI vectors (all
       49 995 000 pairs) equal the oracle's, for the bench's load (F and G),
-      for the CLI's (G only) and for the 8-way row-block split of the
-      multi-GPU path (shard.split_rows, one pfaai_run per block); kernel |E|
-      == the oracle's exact count; sampled rows also compared value by value.
+      for the CLI's (G only), for the 8-way row-block split of the
+      multi-GPU path run over one full load (shard.split_rows, one pfaai_run
+      per block), and for what each rank of an 8-GPU run executes: every
+      block loaded on its own with pfaai_load_rows (the rank's run-end sort,
+      the pass-1 record packing, the block's check) and run, the 8 blocks
+      assembled; kernel |E| == the oracle's exact count; sampled rows also
+      compared value by value.
   C4  query-vs-target, 50 000 targets x 1 000 queries (the -r path, corrected
       semantics): the whole output equals the oracle's; |E| == the oracle's
       count, sampled query rows bit-exact.
@@ -23,9 +27,13 @@ tests assert equality of the entire JAC / AJI vectors
 The generated inputs' digest is compared first, so a generator difference
 between the two machines is reported as such.
   C5  SYN 100 000 x 100 all-vs-all streamed in output tiles (pfaai_stream):
-      tiles arrive in order and cover every pair, 0 <= AJI <= 1 and
-      1 <= N <= P everywhere, sampled rows and their |E| bit-exact against
-      the oracle.
+      the |F| > 2^30 member loads (BIGF), the absolute column windows with
+      k_blk<true>'s per-window run tables and 19 stream tiles; the tiles are
+      fed in JAC order into one running SHA-256 per array, and the whole
+      S / N / AJI vectors (4 999 950 000 pairs, 100 GB) equal the oracle's
+      (make_full_digests.py C5, computed by row windows); |E| equals the
+      oracle's; tiles arrive in order and cover every pair; sampled rows are
+      also compared value by value.
 
 Each case prints progress to $PFAAI_PROGRESS (if set) so a long GPU call is
 never silent.
@@ -156,6 +164,37 @@ def test_c3_10k_all_vs_all_and_8way_rowblocks(engine):
 
 
 @pytest.mark.timeout(300)
+def test_c3_rank_loads_whole_output(engine):
+    """What each GPU of an 8-way run executes (bench.py's ranks,
+    pfaai_group_load): a load of the rank's row block only (pfaai_load_rows:
+    its run-end sort keeps the block's records, builds G_pos / G_end of the
+    block's genomes, checks the block's lists), then pfaai_run of the block.
+    The 8 blocks, each loaded and run on its own, assembled in JAC order,
+    equal the oracle's whole output (reference: distributeGenomePairs,
+    algorithm_impl.hpp:100-120; pfaai_tests.cpp:355-386)."""
+    import torch
+
+    n = 10000
+    pb = _problem("C3")
+    npairs = n * (n - 1) // 2
+    aji = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    S = torch.full((npairs,), -1.0, dtype=torch.float64, device="cuda:0")
+    N = torch.full((npairs,), -1, dtype=torch.int32, device="cuda:0")
+    ev = 0
+    blocks = split_rows(n, 8, cus=256)
+    for rb, re in blocks:
+        engine.load(**pb, rows=(rb, re))
+        engine.run(rb, re, _capi.FLAG_EMIT_JAC, aji.data_ptr(), S.data_ptr(), N.data_ptr(),
+                   stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ev += engine.stats()["n_events"]
+        progress(f"C3 rank block [{rb}, {re}) loaded alone and run")
+    assert ev == DIGESTS["C3"]["events"]
+    assert not (N < 0).any().item()  # every pair written by its block
+    _assert_digests("C3", aji, S, N, "8 rank loads (pfaai_load_rows), assembled")
+
+
+@pytest.mark.timeout(300)
 def test_c4_qt_50000_targets_x_1000_queries(engine):
     nT, nQ, P = 50000, 1000, 100
     t0 = time.time()
@@ -181,44 +220,49 @@ def test_c4_qt_50000_targets_x_1000_queries(engine):
     progress("C4 checked")
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_c5_100k_streamed_tiles(engine):
+    import make_full_digests as mk
+
     n, P = 100000, 100
     t0 = time.time()
-    g = syn.generate(n, P)
-    pb = dict(mode=_capi.MODE_ALL, n_ids=n, n_prot=P, Lp=g["Lp"], F_prot=g["F_prot"], F_genome=g["F_genome"],
-              T=g["T"], G_off=g["G_off"], G_tet=g["G_tet"])
-    progress(f"C5 generated in {time.time() - t0:.1f}s (|F| = {len(g['F_genome'])})")
+    pb = _problem("C5")
+    progress(f"C5 generated + input digest in {time.time() - t0:.1f}s (|F| = {len(pb['F_genome'])})")
     engine.load(**pb)
     progress(f"C5 loaded at {time.time() - t0:.1f}s")
-    pr = O.Problem(pb)
     n_rows, npairs = engine.shape()
-    sample = [0, 1, 31337, 77777, n - 2]
+    sample = [0, 31337, n - 2]
     got = {}
     seen = []
     bad = []
+    rd = mk.RunningDigests()
 
     def sink(rb, re, first, a, s, nn):
         if seen and seen[-1][1] != rb:
             bad.append(("order", rb))
+        if first != rd.pairs:
+            bad.append(("first", rb, first, rd.pairs))
         seen.append((rb, re, first, len(a)))
-        if not ((a > 0) & (a <= 1)).all() or not ((nn >= 1) & (nn <= P)).all():
-            bad.append(("range", rb))
+        rd.update(s, nn, a)  # JAC order: one running SHA-256 per array
         for r in sample:
             if rb <= r < re:
                 f, c = engine.row_span(r, r + 1)
                 got[r] = (a[f - first: f - first + c].copy(), s[f - first: f - first + c].copy(),
                           nn[f - first: f - first + c].copy())
-        if len(seen) % 4 == 0:
-            progress(f"C5 tile {len(seen)} rows [{rb}, {re})")
+        progress(f"C5 tile {len(seen)} rows [{rb}, {re}) hashed")
         return 0
 
     ne = engine.stream(0, n_rows, 1 << 28, _capi.FLAG_EMIT_JAC, sink)
-    progress(f"C5 streamed {len(seen)} tiles at {time.time() - t0:.1f}s")
+    progress(f"C5 streamed and hashed {len(seen)} tiles at {time.time() - t0:.1f}s")
+    assert engine.stats()["rows_kernel"] == "pl"
     assert not bad, bad[:5]
     assert seen[0][0] == 0 and seen[-1][1] == n_rows and len(seen) > 1
-    assert sum(x[3] for x in seen) == npairs
-    assert ne == pr.count_e()  # |E| over all 5e9 pairs = the reference's count
+    assert sum(x[3] for x in seen) == npairs == rd.pairs
+    assert ne == DIGESTS["C5"]["events"]  # |E| over all 5e9 pairs = the reference's count
+    want = DIGESTS["C5"]["sha256"]
+    assert rd.hexdigests() == want, f"C5 whole output differs from the oracle's"
+    progress("C5: whole output equals the oracle's")
+    pr = O.Problem(pb)
     for r in sample:
         a, s, nn = got[r]
         f, _ = engine.row_span(r, r + 1)

@@ -29,7 +29,7 @@ def syn_problem():
     return ds, ref
 
 
-@pytest.mark.parametrize("variant", ["pl", "v2", "pl512", "fused", "worklist"])
+@pytest.mark.parametrize("variant", ["pl", "pl512", "fused", "worklist"])
 def test_row_kernel_variants(diag_engine, syn_problem, variant):
     ds, ref = syn_problem
     os.environ["PFAAI_ROWS_KERNEL"] = variant
