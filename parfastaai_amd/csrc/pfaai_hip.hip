@@ -732,9 +732,13 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
         hipLaunchKernelGGL(k_tnz, dim3(ceil_div(kNTetramers, 256)), dim3(256), 0, s, rho, flag);
     }
     const uint32_t mask1 = (1u << DB) - 1u, mask2 = (1u << hb) - 1u;
+    // the WK 3 member codes (k_fcode's), written by the histogram pass
+    if (int rc = ensure(c, c->Fcode, (size_t)(n_f + 16) * sizeof(uint32_t))) return rc;
+    HIPCHK(c, hipMemsetAsync(static_cast<uint32_t*>(c->Fcode.p) + n_f, 0, 16 * sizeof(uint32_t), s));
     hipLaunchKernelGGL((k_fends_hist<DB, NT>), dim3(ntiles), dim3(NT), 0, s, Fp, Fg, bend, n_f, (uint32_t)P, g_lo, g_hi,
                        mask1, static_cast<uint16_t*>(c->Fp16.p), D, hist, ftail, ltail, trank, flag,
-                       seeds ? seeds[0] : 0ull, seeds ? seeds[1] : 0ull, seeds ? hpart : nullptr);
+                       seeds ? seeds[0] : 0ull, seeds ? seeds[1] : 0ull, seeds ? hpart : nullptr,
+                       static_cast<uint32_t*>(c->Fcode.p));
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL(k_tail_suffix, dim3((int)std::min<int64_t>(ceil_div(ntiles, 256), 4096)), dim3(256), 0, s, ftail,
                        ntiles, ntail);
@@ -1314,13 +1318,16 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
                 HIPCHK(c, hipGetLastError());
             }
         }
-        // member codes for the WK 3 walks (all-vs-all with G_pos / G_end)
+        // member codes for the WK 3 walks (all-vs-all with G_pos / G_end):
+        // the run-end sort's histogram pass wrote them; else k_fcode
         d.Fcode = nullptr;
         if (d.G_end && p.mode == PFAAI_MODE_ALL) {
-            if ((rc = ensure(c, c->Fcode, (size_t)(n_f + 16) * sizeof(uint32_t)))) return rc;
-            hipLaunchKernelGGL(k_fcode, dim3((int)std::min<int64_t>(ceil_div(n_f + 16, 256), 1 << 16)), dim3(256), 0, s,
-                               d.Fg, n_f, static_cast<uint32_t*>(c->Fcode.p));
-            HIPCHK(c, hipGetLastError());
+            if (!ends_built) {
+                if ((rc = ensure(c, c->Fcode, (size_t)(n_f + 16) * sizeof(uint32_t)))) return rc;
+                hipLaunchKernelGGL(k_fcode, dim3((int)std::min<int64_t>(ceil_div(n_f + 16, 256), 1 << 16)), dim3(256), 0,
+                                   s, d.Fg, n_f, static_cast<uint32_t*>(c->Fcode.p));
+                HIPCHK(c, hipGetLastError());
+            }
             d.Fcode = static_cast<const uint32_t*>(c->Fcode.p);
         } else {
             release(c->Fcode);

@@ -9,14 +9,12 @@
 namespace pfaai_impl {
 
 // k_rows_pl's variant bits for the WK 3 walks (pfaai_rows_pl.hpp V): the
-// release forms kPlV (1024 threads) and 0 (the 512-thread narrow rows);
-// PFAAI_PL_V=0..3 overrides both (diagnostics, A/B).
-constexpr int kPlV = 3;
-template <int NT>
-inline int pl_v() {
-    const char* v = DIAG_ENV("PFAAI_PL_V");
-    return v ? std::max(0, std::min(3, atoi(v))) : NT == 1024 ? kPlV : 0;
-}
+// release form kPlV; PFAAI_PL_V=0, 3, 19, 25 overrides it (diagnostics, A/B).
+// The other forms (column windows, -q, -r, full rows) take kPlVG's S5 bits
+// where they do not spill (MODE 2 compiles both S5 forms: 114 VGPRs spilled,
+// so -r keeps V 0); PFAAI_PL_VG=0 overrides (A/B).
+constexpr int kPlV = 27;
+constexpr int kPlVG = 9;
 
 template <int MODE, int KW, int NT, int WPE, int NK>
 void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
@@ -39,23 +37,39 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, WKV, VV>), dim3(r1 - r0, gy), dim3(NT), lds, s, \
                        dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
         c->last_walk = gp ? PFAAI_WALK_GPOS : PFAAI_WALK_SPLITTERS;
+        constexpr int VG = MODE == 2 ? 0 : kPlVG;
+        const bool vg = VG != 0 && !(DIAG_ENV("PFAAI_PL_VG") && atoi(DIAG_ENV("PFAAI_PL_VG")) == 0);
         if (wk == 0 || abs_chunk >= 0) {
             c->last_walk = PFAAI_WALK_SPLITTERS;
-            if (bigf) PLK(true, 0, 0); else PLK(false, 0, 0);
+            if (vg) {
+                if (bigf) PLK(true, 0, VG); else PLK(false, 0, VG);
+            } else {
+                if (bigf) PLK(true, 0, 0); else PLK(false, 0, 0);
+            }
         } else if constexpr (kWk1 != 0) {
             if constexpr (MODE == 0) {
                 if (gp) {  // (G_pos is built up to 20 480 genomes only: never BIGF)
                     if (bigf) { PLK(true, 3, 0); return; }
-                    switch (pl_v<NT>()) {
-                        case 1: PLK(false, 3, 1); break;
-                        case 2: PLK(false, 3, 2); break;
-                        case 3: PLK(false, 3, 3); break;
-                        default: PLK(false, 3, 0); break;
+#ifdef PFAAI_DIAGNOSTICS
+                    if (const char* v = DIAG_ENV("PFAAI_PL_V")) {
+                        switch (atoi(v)) {
+                            case 0: PLK(false, 3, 0); return;
+                            case 3: PLK(false, 3, 3); return;
+                            case 19: PLK(false, 3, 19); return;
+                            case 25: PLK(false, 3, 25); return;
+                            default: break;
+                        }
                     }
+#endif
+                    PLK(false, 3, kPlV);
                     return;
                 }
             }
-            if (bigf) PLK(true, kWk1, 0); else PLK(false, kWk1, 0);
+            if (vg) {
+                if (bigf) PLK(true, kWk1, VG); else PLK(false, kWk1, VG);
+            } else {
+                if (bigf) PLK(true, kWk1, 0); else PLK(false, kWk1, 0);
+            }
         }
 #undef PLK
     };

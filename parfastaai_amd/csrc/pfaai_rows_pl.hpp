@@ -138,6 +138,24 @@ __device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __rest
     return mask;
 }
 
+// c0 / d0 and c1 / d1 with one v_rcp_f64 (V bit 8): Y ~ 1 / (d0 d1) (the
+// product is exact: d < 2^17), one Newton step, then y0 = d1 Y ~ 1 / d0 and
+// y1 = d0 Y ~ 1 / d1 (relative error ~2^-44), and per column q = c y and the
+// residual correction -- whose result is then within ~2^-88 of c / d,
+// closer than any rounding boundary (>= 2^-54 / d away), i.e. IEEE c / d.
+// Checked on the device by pfaai_debug_div_check's pair mode.  Needs d >= 1
+// (S5 clamps a zero counter's d to 1).  One v_rcp_f64 (~17 cycles of issue)
+// and a Newton step fewer per word for one more multiply.
+__device__ __forceinline__ void exact_div_pair(int32_t c0, int32_t d0i, int32_t c1, int32_t d1i, double& s0, double& s1) {
+    const double d0 = (double)d0i, d1 = (double)d1i, pd = d0 * d1;
+    double y = __builtin_amdgcn_rcp(pd);
+    y = __builtin_fma(y, __builtin_fma(-pd, y, 1.0), y);
+    const double y0 = d1 * y, a0 = (double)c0 * y0;
+    s0 += __builtin_fma(__builtin_fma(-d0, a0, (double)c0), y0, a0);
+    const double y1 = d0 * y, a1 = (double)c1 * y1;
+    s1 += __builtin_fma(__builtin_fma(-d1, a1, (double)c1), y1, a1);
+}
+
 // WK 3 member scatter of a lane's 8 member codes (k_fcode: counter word
 // byte offset code >> 5, u16 half increment 1 << code) under the lane's
 // mask bits m: per member one v_cmpx sets EXEC to the lanes holding it, three
@@ -188,13 +206,20 @@ constexpr int kClkBlocks = 256;
 // behind the member atomics in LDS.)
 // V (variant bits): 1 S5 divides both columns of a nonzero counter word (no
 // per-column branches: the SALU of six exec-mask updates per word); 2 the
-// WK 3 member scatter by pl_scatter8_code over k_fcode's member codes.  The
-// 1024-thread WK 3 launches take V = 3 (pfaai_launch.hpp kPlV; 10k
-// all-vs-all 8.11-8.24 -> 8.07 ms in tools/gpu/ab_rows.py, profiles/r05c,
-// r05d); the 512-thread narrow launch keeps V = 0 (V 2 / 3 spill there:
-// 1.09 -> 1.12 ms).  Giving the S1-S3 entries to the last waves and the extra
-// member rounds to the middle ones (a per-wave balance) measured slower:
-// 8.11 -> 8.28 ms.
+// WK 3 member scatter by pl_scatter8_code over k_fcode's member codes; 8
+// S5's two divisions of a word by one reciprocal (exact_div_pair, with 1);
+// 16 the G entries one protein ahead instead of two (WK 3, ONE below).  The
+// WK 3 launches take V = 27 (pfaai_launch.hpp kPlV), the other forms V = 0.
+// Measured (tools/gpu/ab_rows.py, 10k all-vs-all, single launches of the
+// diagnostics build, profiles/r05/ab_v_*.txt): V 0 -> 3: 8.11-8.24 -> 8.07
+// ms; 3 -> 19: 8.16 -> 7.91; 3 -> 27: 8.16 -> 7.84 (the first 894 rows 1.148
+// -> 1.099, the 512-thread narrow rows alone 1.087 -> 1.054 at V 0 -> 27);
+// V 2 alone on the narrow rows spilled (1.09 -> 1.12 ms) until V 16 freed
+// two VGPRs, and so did V 8 without V 16 (a 16-B spill of two accumulators
+// per protein).  Rejected: a guard-free member issue (both 16-B loads at the
+// task's offsets whatever the mask, the mask by one v_bfi: 8.08 -> 8.30 ms,
+// it spilled); the S1-S3 entries on the last waves and the extra member
+// rounds on the middle ones (a per-wave balance): 8.11 -> 8.28.
 template <int MODE, int KW, int NT, int WPE = 4, bool CLK = false, int NK = 0, bool BIGF = false, int WK = 0,
           int V = 0>
 __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, int32_t chunk_cols, int32_t abs_chunk,
@@ -323,7 +348,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             }
         }
     };
-    auto s3 = [&](int q, const uint4 (&r4)[EPT], const uint32_t (&gq2)[EPT]) {  // line tasks of protein q
+    // ONE (WK 3, V bit 16): the G entries' (G_pos, G_end) are loaded one
+    // protein ahead and cut straight from the S1 registers -- S2 is only a
+    // register copy under WK 3, and its second stage holds 2 VGPRs across the
+    // whole iteration
+    constexpr bool ONE = GP && (V & 16) != 0;
+    auto s3 = [&](int q, const uint4 (&r4)[EPT], const uint32_t (&gq2)[EPT], const int32_t (&gt1)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
         if (wbase0 >= glen(q)) return;
         uint32_t nl[EPT], v = 0;
@@ -332,7 +362,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             const int e = tid + j * NT;
             uint2 r;
             if constexpr (GP) {
-                r = make_uint2(gq2[j] + 1u, r4[j].y);  // OOB entries: (1, 0), empty
+                r = make_uint2(gq2[j] + 1u, ONE ? (uint32_t)gt1[j] : r4[j].y);  // OOB entries: (1, 0), empty
                 nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
             } else {
                 nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && abs_chunk >= 0));
@@ -379,12 +409,18 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     uint32_t gq[EPT], gq2[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) { r4[j] = make_uint4(0u, 0u, 0u, 0u); gq[j] = gq2[j] = 0u; }
-    s1(0, gt, gq);
-    s2(0, gt, r4, gq, gq2);
-    s1(1, gt, gq);
-    s3(0, r4, gq2);
-    s2(1, gt, r4, gq, gq2);
-    s1(2, gt, gq);
+    if constexpr (ONE) {
+        s1(0, gt, gq);
+        s3(0, r4, gq, gt);
+        s1(1, gt, gq);
+    } else {
+        s1(0, gt, gq);
+        s2(0, gt, r4, gq, gq2);
+        s1(1, gt, gq);
+        s3(0, r4, gq2, gt);
+        s2(1, gt, r4, gq, gq2);
+        s1(2, gt, gq);
+    }
     __syncthreads();
 
     unsigned long long ck[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -431,8 +467,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     n_add(k, v);
                     const int32_t d0 = max(ta + (int32_t)(tw[k] & 0xFFFFu) - c0, 1);
                     const int32_t d1 = max(ta + (int32_t)(tw[k] >> 16) - c1, 1);
-                    S[2 * k] += exact_div_small((double)c0, (double)d0);
-                    S[2 * k + 1] += exact_div_small((double)c1, (double)d1);
+                    if constexpr ((V & 8) != 0) {
+                        exact_div_pair(c0, d0, c1, d1, S[2 * k], S[2 * k + 1]);
+                    } else {
+                        S[2 * k] += exact_div_small((double)c0, (double)d0);
+                        S[2 * k + 1] += exact_div_small((double)c1, (double)d1);
+                    }
                 }
             }
             return;
@@ -494,10 +534,16 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t okm = issue2(grpx, nt, b, bh);
         stamp(0);
         // S3(i+1), then the prefetches S2(i+2), S1(i+3)
-        if (i + 1 < P) s3(i + 1, r4, gq2);
-        stamp(1);
-        s2(i + 2, gt, r4, gq, gq2);
-        s1(i + 3, gt, gq);
+        if constexpr (ONE) {
+            if (i + 1 < P) s3(i + 1, r4, gq, gt);
+            stamp(1);
+            s1(i + 2, gt, gq);
+        } else {
+            if (i + 1 < P) s3(i + 1, r4, gq2, gt);
+            stamp(1);
+            s2(i + 2, gt, r4, gq, gq2);
+            s1(i + 3, gt, gq);
+        }
         stamp(2);
         if (prio) __builtin_amdgcn_s_setprio(0);
         stamp(3);

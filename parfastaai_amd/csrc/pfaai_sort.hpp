@@ -303,7 +303,11 @@ __global__ void k_tnz(const unsigned long long* __restrict__ rho, uint32_t* __re
 
 // Pass 1's histogram over F (kept records only) + the u16 protein column +
 // each entry's distance to its run end (D) + the tile's first run end
-// (ftail, absolute).  Every global load is issued before the first store.
+// (ftail, absolute) + (code, nullable) the member codes of k_fcode for every
+// entry, kept or not (the row kernel's members are any genome): the tile's
+// genome ids are in registers anyway, so the codes cost one store per entry
+// here against a 0.49 ms pass over Fg at 10k.  Every global load is issued
+// before the first store.
 template <int DB, int NT>
 __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ Fp, const int32_t* __restrict__ Fg,
                                                    const uint32_t* __restrict__ bend, int64_t n, uint32_t P,
@@ -313,7 +317,8 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
                                                    uint32_t* __restrict__ ltail,
                                                    const unsigned long long* __restrict__ trank,
                                                    const uint32_t* __restrict__ tnz, uint64_t seed,
-                                                   uint64_t seed2, unsigned long long* __restrict__ hpart) {
+                                                   uint64_t seed2, unsigned long long* __restrict__ hpart,
+                                                   uint32_t* __restrict__ code) {
     constexpr int BINS = 1 << DB, kTile = NT * kSortItems, kChunks = kTile / 64;
     static_assert(kChunks <= 64, "one wave ballots the tile's chunks");
     __shared__ uint32_t h[BINS];
@@ -341,6 +346,7 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
     const int rn = (int)min<int64_t>(kTile, n - t0);
     const rsrc_t r_p = mk_rsrc(Fp + t0, (uint64_t)rn * 4u), r_g = mk_rsrc(Fg + t0, (uint64_t)rn * 4u);
     const rsrc_t r_fp16 = mk_rsrc(fp16 ? fp16 + t0 : nullptr, fp16 ? (uint64_t)rn * 2u : 0u);
+    const rsrc_t r_code = mk_rsrc(code ? code + t0 : nullptr, code ? (uint64_t)rn * 4u : 0u);
     const uint32_t gspan = (uint32_t)(g_hi - g_lo);
     int32_t p[kSortItems], g[kSortItems];
 #pragma unroll
@@ -357,6 +363,10 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
         const int r = k * NT + tid;
         sp[r] = (uint16_t)p[k];
         if (fp16) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)p[k], r_fp16, r * 2, 0, 0);
+        if (code) {
+            const uint32_t b = (uint32_t)g[k];
+            __builtin_amdgcn_raw_buffer_store_b32(((b >> 1) << 7) | ((b & 1u) << 4), r_code, r * 4, 0, 0);
+        }
         if (r < rn && (uint32_t)(g[k] - g_lo) < gspan) atomicAdd(&h[((uint32_t)g[k] * P + (uint32_t)p[k]) & mask], 1u);
     }
     if (tid < kTile / 32) sb[tid] = bw;

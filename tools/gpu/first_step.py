@@ -1,14 +1,21 @@
 """The first pfaai_run after a load against the next ones (device time of
-each, eng.timing), 10k all-vs-all: does the first carry a one-time cost?
+each, eng.timing), 10k all-vs-all: does the first carry a one-time cost, and
+is it the load or the idle time before the run?
 
     python tools/gpu/first_step.py [n] [--busy]
 
---busy: keep the GPU busy (torch matmuls, ~50 ms) right before each load, to
-tell a clock ramp from a cold cache / TLB.
+Cases (each a list of consecutive run times, ms):
+  after_load          load, then 4 runs (rounds 3-4's observation: 7.9, 7.6, 7.4)
+  after_idle_<ms>     steady runs, the host sleeps <ms>, then 4 runs
+  after_load_spin     load, a ~30 ms torch matmul spin, then 4 runs
+  after_idle_spin     steady runs, 200 ms sleep, the spin, then 4 runs
+--busy: also keep the GPU busy (torch matmuls, ~50 ms) right before each load
+(round 4's test).
 """
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
@@ -22,22 +29,47 @@ n = int(args[0]) if args else 10000
 g = syn.generate(n, 100)
 ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
 eng = _capi.Engine(0)
-out = {"deferred_env": os.environ.get("HIP_ENABLE_DEFERRED_LOADING"), "busy": busy}
-for rep in range(2):
-    if busy:
-        a = torch.randn(4096, 4096, device="cuda:0")
-        for _ in range(40):
+out = {"busy": busy}
+
+
+def spin(ms=30.0):
+    """Dense matmuls on the context's device for about ms."""
+    a = torch.randn(4096, 4096, device="cuda:0")
+    t0 = time.time()
+    while (time.time() - t0) * 1e3 < ms:
+        for _ in range(4):
             a = a @ a
             a = a / a.norm()
         torch.cuda.synchronize()
-    eng.load(**ds.problem())
-    rows, pairs = eng.shape()
-    d = eng.alloc(pairs * 8) if rep == 0 else d
+
+
+def runs(k=4):
     ts = []
-    for _ in range(4):
+    for _ in range(k):
         eng.timing(reset=True)
         eng.run(0, rows, 0, d)
         _, b, r = eng.timing(reset=True)
         ts.append(round(b + r, 3))
-    out[f"load{rep}_runs_ms"] = ts
+    return ts
+
+
+d = None
+for rep in range(2):
+    if busy:
+        spin(50)
+    eng.load(**ds.problem())
+    rows, pairs = eng.shape()
+    d = eng.alloc(pairs * 8) if d is None else d
+    out[f"after_load{rep}"] = runs()
+for idle in (20, 200, 1000):
+    runs(3)
+    time.sleep(idle / 1e3)
+    out[f"after_idle_{idle}ms"] = runs()
+eng.load(**ds.problem())
+spin(30)
+out["after_load_spin"] = runs()
+runs(3)
+time.sleep(0.2)
+spin(30)
+out["after_idle_spin"] = runs()
 print(json.dumps(out), flush=True)

@@ -15,10 +15,16 @@
 #ifndef WKP
 #define WKP 3
 #endif
+#ifndef MODEP
+#define MODEP 0
+#endif
+#ifndef BIGFP
+#define BIGFP false
+#endif
 #ifndef VP
 #define VP 0
 #endif
 
-template __global__ void pfaai::k_rows_pl<0, KWP, NTP, 8, false, NKP, false, WKP, VP>(
+template __global__ void pfaai::k_rows_pl<MODEP, KWP, NTP, 8, false, NKP, BIGFP, WKP, VP>(
     pfaai::Dev, int64_t, int32_t, int32_t, uint32_t, const unsigned long long*, double*, double*, int32_t*,
     unsigned long long*, unsigned long long*);
