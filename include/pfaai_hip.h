@@ -336,9 +336,11 @@ int pfaai_timing(pfaai_ctx* ctx, int reset, int32_t* n_runs, double* ms_build,
 int pfaai_debug_row_counts(pfaai_ctx* ctx, int64_t row, int32_t* h_counts);
 
 /* Self-test of the row kernels' exact small-integer division: compares
- * c / d computed by the fast path with IEEE '/' for every 1 <= c <= c_max,
- * c <= d <= d_max on the device; *mismatches receives the count (0 = every
- * quotient bit-identical). */
+ * c / d computed by the fast paths with IEEE '/' for every 1 <= c <= c_max,
+ * c <= d <= d_max on the device -- exact_div_small, and the paired form of
+ * k_rows_pl's S5 (one reciprocal for two columns) with six partner
+ * denominators per (c, d), both of its columns checked; *mismatches receives
+ * the count (0 = every quotient bit-identical). */
 int pfaai_debug_div_check(pfaai_ctx* ctx, int32_t c_max, int32_t d_max, int64_t* mismatches);
 
 /* Diagnostics: per-stage shader-clock sums of k_rows_pl (PFAAI_PL_CLK=1,

@@ -27,7 +27,10 @@
 // rows Z and Q).  The explicit forms choose the mode, the corrected
 // semantics (ref_compat = false) and the device(s).
 #pragma once
+#include <sys/mman.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <exception>
@@ -73,10 +76,23 @@ inline CtxPtr make_ctx(int device) {
 }
 
 // [0, n) over up to 16 host threads (the adapter's array conversions)
+// Ask for transparent huge pages on a large allocation nothing has touched
+// yet: its first touch then faults 2-MB pages instead of 4-KB ones (the
+// CLI's C2 output arrays, 64 MB, took ~15 ms of page faults at 4 KB,
+// serialised in the kernel's page-table lock however many threads touch
+// them).  A hint: no effect where THP is off.
+inline void advise_huge(const void* p, std::size_t bytes) {
+    const auto a = (reinterpret_cast<std::uintptr_t>(p) + (((std::uintptr_t)1 << 21) - 1)) & ~(((std::uintptr_t)1 << 21) - 1);
+    const auto e = reinterpret_cast<std::uintptr_t>(p) + bytes;
+    if (e > a + ((std::uintptr_t)1 << 21)) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+}
+
 template <class Fn>
 void par_range(int64_t n, Fn fn) {
+    // >= 64k elements per thread (a 2M-pair JAC fill ran on one thread at the
+    // old 4M grain: round-4's C2 "D2H / JAC fill" 25.5 ms)
     const int nt = (int)std::max<int64_t>(
-        1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 22}));
+        1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
     std::vector<std::thread> th;
     int started = 0;
     try {
@@ -209,20 +225,31 @@ class ParFAAIHipImpl {
     int computeJAC() {
         // the reference's own initJAC (the genome ids of every pair) runs on
         // a host thread while the device computes S / N / AJI
+        const auto t0 = std::chrono::steady_clock::now();
+        auto ms_since = [](std::chrono::steady_clock::time_point t) {
+            return (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+        };
         int64_t rows = 0, pairs = 0;
         pfaai_shape(ctx(), &rows, &pairs);
         const std::size_t n = (std::size_t)pairs;
         std::unique_ptr<double[]> S(new double[n ? n : 1]);  // no value-initialisation: the device fills them
         std::unique_ptr<int32_t[]> N(new int32_t[n ? n : 1]);
+        detail::advise_huge(S.get(), n * sizeof(double));
+        detail::advise_huge(N.get(), n * sizeof(int32_t));
+        m_AJIdev.clear();
+        m_AJIdev.shrink_to_fit();
+        m_AJIdev.reserve(n);  // (untouched: huge pages before the zero fill)
+        detail::advise_huge(m_AJIdev.data(), n * sizeof(double));
         m_AJIdev.resize(n);
         const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
         std::thread ids;
         bool ids_async = true;
         std::exception_ptr ids_err;  // initJAC's exception, rethrown on this thread
         try {
-            ids = std::thread([this, &ids_err] {
+            ids = std::thread([this, &ids_err, t0, ms_since] {
                 try {
                     m_JAC = m_ds.initJAC();
+                    m_msIds = ms_since(t0);
                 } catch (...) {
                     ids_err = std::current_exception();
                 }
@@ -244,7 +271,9 @@ class ParFAAIHipImpl {
             if (ids_async) ids.join();
             throw;
         }
+        m_msCompute = ms_since(t0);
         if (ids_async) ids.join();
+        const auto t_fill = std::chrono::steady_clock::now();
         if (ids_err) std::rethrow_exception(ids_err);
         if (rc) throw HipError(rc, err);
         if (m_JAC.size() != n) throw HipError(PFAAI_RC_INVALID, "initJAC size differs from the engine's pair count");
@@ -260,6 +289,7 @@ class ParFAAIHipImpl {
                 m_JAC[i].N = N[i];
             }
         });
+        m_msFill = ms_since(t_fill);
         if (m_ctx.size() == 1) {
             pfaai_last_stats(ctx(), &m_events, &m_msBuild, &m_msRows);
             pfaai_run_info(ctx(), &m_rowsKernel, nullptr);
@@ -269,8 +299,16 @@ class ParFAAIHipImpl {
     }
     // algorithm_impl.hpp:309-322 (the kernel epilogue already divided S / N)
     int computeAJI() {
-        if (m_AJIdev.size() != m_JAC.size() || m_JAC.empty()) computeJAC();
-        m_AJI.assign(m_AJIdev.begin(), m_AJIdev.end());
+        if (m_AJIdev.size() != m_JAC.size() || m_JAC.empty()) {
+            if (!m_JAC.empty() && m_AJI.size() == m_JAC.size()) return 0;  // already moved out
+            computeJAC();
+        }
+        if constexpr (std::is_same<ValueType, double>::value) {
+            m_AJI.swap(m_AJIdev);  // the device's AJI as it landed (no 8 B-per-pair copy)
+            m_AJIdev.clear();
+        } else {
+            m_AJI.assign(m_AJIdev.begin(), m_AJIdev.end());
+        }
         return 0;
     }
     // algorithm_impl.hpp:325-329
@@ -328,6 +366,12 @@ class ParFAAIHipImpl {
                         (double)m_AJI[i]);
     }
     int64_t nEvents() const { return m_events; }
+    // host-side times (ms) of the last computeJAC, from its start: initJAC
+    // done (on its thread), the engine's compute + D2H done; and the JAC
+    // tuple fill after both
+    float msIds() const { return m_msIds; }
+    float msCompute() const { return m_msCompute; }
+    float msFill() const { return m_msFill; }
     float msBuild() const { return m_msBuild; }
     float msRows() const { return m_msRows; }
     int mode() const { return m_mode; }
@@ -450,6 +494,7 @@ class ParFAAIHipImpl {
     std::vector<uint8_t> m_isq;
     std::vector<JACType> m_JAC;
     std::vector<double> m_AJIdev;
+    float m_msIds = 0.f, m_msCompute = 0.f, m_msFill = 0.f;
     std::vector<ValueType> m_AJI;
     int64_t m_events = 0;
     float m_msBuild = 0.f, m_msRows = 0.f;

@@ -85,6 +85,14 @@ __global__ void k_fp16(const int32_t* __restrict__ Fp, int64_t n, uint16_t* __re
         Fp16[i] = (uint16_t)Fp[i];
 }
 
+// (G_pos, G_end) -> the interleaved G_pe the WK 3 walks read (the fallback
+// builds, whose G_pos and G_end come from different kernels)
+__global__ void k_pack_pe(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ end, int64_t n,
+                          uint2* __restrict__ pe) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        pe[i] = make_uint2(pos[i], end[i]);
+}
+
 // Member codes of F for k_rows_pl's WK 3 member scatter: genome b as
 // (b >> 1) << 7 | (b & 1) << 4, so that the counter word's LDS byte offset
 // is code >> 5 and the u16 half's increment is 1 << code (a VALU shift reads

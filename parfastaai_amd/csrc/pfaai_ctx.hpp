@@ -62,7 +62,8 @@ struct pfaai_ctx {
     int64_t max_glen = 0;  // longest (genome, protein) G list
     DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, G_pos, blk;
-    DevBuf G_end;  // end of the F run of every G entry (with G_pos; k_rows_pl WK 3)
+    DevBuf G_end;  // end of the F run of every G entry (the fallback builds, packed into G_pe)
+    DevBuf G_pe;   // (G_pos, G_end) of every G entry, interleaved: what k_rows_pl WK 3 reads
     DevBuf Fcode;  // member codes of F (k_fcode; with G_end, the WK 3 member scatter)
     bool has_g = false;
     bool runs_valid = false;  // run table (and, if runs_key, the first E key) built for the loaded problem
@@ -95,6 +96,10 @@ struct pfaai_ctx {
     hipEvent_t narrow_ev[2] = {nullptr, nullptr};
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
+    // staged D2H of host outputs (pfaai_compute / pfaai_compute_rows): two
+    // pinned chunks and their events (d2h_staged)
+    void* d2h_host = nullptr;
+    hipEvent_t d2h_ev[2] = {nullptr, nullptr};
     // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
     hipStream_t copy_stream = nullptr;
     hipEvent_t st_done[2] = {nullptr, nullptr}, st_copied[2] = {nullptr, nullptr};
@@ -221,7 +226,7 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
 // (k_blk_end) instead of k_blk's 16-B entries.  One predicate for the run
 // table build (run_mode) and the kernel choice (launch_pl).
 inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
-    return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pos && !c->windows &&
+    return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pe && !c->windows &&
            c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
            !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");

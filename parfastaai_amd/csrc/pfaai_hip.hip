@@ -53,6 +53,49 @@ int par_for(int64_t n, Fn fn, int64_t work = -1) {
 // exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
 
+// Device -> caller's host memory for the host-output entry points: chunks of
+// kD2hChunk bytes through two pinned buffers, the copy of chunk i overlapping
+// the host threads' memcpy of chunk i - 1 into dst.  A plain hipMemcpyAsync
+// into pageable memory that nothing has touched yet ran at ~2.5 GB/s (the
+// CLI's C2 outputs, 40 MB: 16 ms of its 18 ms pfaai_compute, round 5); the
+// pinned copies run at the link's rate and the page faults of dst are taken
+// by 16 threads at once.  Work ordered before on stream s is waited for.
+// The pinned pair is allocated by pfaai_create (a 64 MB hipHostMalloc at the
+// first compute cost the CLI's C2 run ~18 ms; at create it runs on the CLI's
+// helper thread beside the SQLite read).
+constexpr size_t kD2hChunk = (size_t)8 << 20;
+int d2h_staged(pfaai_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return PFAAI_RC_OK;
+    if (bytes < ((size_t)4 << 20)) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        return PFAAI_RC_OK;
+    }
+    if (!c->d2h_host) HIPCHK(c, hipHostMalloc(&c->d2h_host, 2 * kD2hChunk, hipHostMallocDefault));
+    for (hipEvent_t& e : c->d2h_ev)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t nch = (bytes + kD2hChunk - 1) / kD2hChunk;
+    auto* h = static_cast<char*>(c->d2h_host);
+    auto host_copy = [&](size_t k) -> int {
+        const size_t off = k * kD2hChunk, len = std::min(kD2hChunk, bytes - off);
+        HIPCHK(c, hipEventSynchronize(c->d2h_ev[k & 1]));
+        char* d = static_cast<char*>(dst) + off;
+        const char* b = h + (k & 1) * kD2hChunk;
+        par_for((int64_t)len, [&](int64_t lo, int64_t hi, int) { std::memcpy(d + lo, b + lo, (size_t)(hi - lo)); });
+        return PFAAI_RC_OK;
+    };
+    for (size_t k = 0; k < nch; ++k) {
+        const size_t off = k * kD2hChunk, len = std::min(kD2hChunk, bytes - off);
+        HIPCHK(c, hipMemcpyAsync(h + (k & 1) * kD2hChunk, static_cast<const char*>(src) + off, len,
+                                 hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipEventRecord(c->d2h_ev[k & 1], s));
+        if (k >= 1) {  // chunk k - 1 to dst while chunk k is copied; buffer (k + 1) & 1 is then free
+            if (int rc = host_copy(k - 1)) return rc;
+        }
+    }
+    return host_copy(nch - 1);
+}
+
 // Sort space for n keys: two key and two value ping-pong buffers, the
 // per-tile digit histograms and their scan (k_rs_hist / k_rs_scatter).
 int ensure_sort_space(pfaai_ctx* c, int64_t n) {
@@ -347,8 +390,8 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     } else if (wl) {
         rc = build_records<MODE>(c, rb, re, s, compat);
     }
-    if (!wl && ends && c->dev.G_end) {
-        // WK 3 reads G_end (built at load): no run table; only the ref-compat
+    if (!wl && ends && c->dev.G_pe) {
+        // WK 3 reads G_pe (built at load): no run table; only the ref-compat
         // zero-overlap quirk's first E triple
         if (compat) rc = launch_first_key(c, s);
     } else if (!wl && !keep) {
@@ -768,8 +811,7 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
         hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ng2, base, tctr);
         hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>),
                            dim3((int)std::min<int64_t>(nt2, (int64_t)cus * std::max(1, per2))), dim3(NT), lds, s, src2,
-                           DstGposEnds{static_cast<uint32_t*>(c->G_pos.p) + gbase, static_cast<uint32_t*>(c->G_end.p) + gbase,
-                                       hb},
+                           DstGposEnds{static_cast<uint2*>(c->G_pe.p) + gbase, hb},
                            n_kept, nt2, 0, mask2, hist, gsum, base, tctr);
         HIPCHK(c, hipGetLastError());
     }
@@ -1136,13 +1178,13 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
     // for 7.8 ms of kernels at 10k)
     if (in_g && in_f && n_f && n_g == n_f && ng < ((int64_t)1 << 32)) {
         if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
-        if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if (want_pos && (rc = ensure(c, c->G_pe, n_f * sizeof(uint2)))) return rc;
         if (want_pos && (rc = ensure_gpos_ends_pre(c, n_f, n_kept, ng))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     } else if (in_g && !in_f && n_f && P < kMaxRuns && ng < ((int64_t)1 << 32)) {  // G only: both sorts' buffers
         if ((rc = ensure_tsort(c, n_f, 18, true))) return rc;
         if (want_pos && (rc = ensure_tsort(c, n_f, bits_for(ng), false))) return rc;
-        if (want_pos && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+        if (want_pos && (rc = ensure(c, c->G_pe, n_f * sizeof(uint2)))) return rc;
         if (want_pos && (rc = ensure_gpos_ends_pre(c, n_f, n_kept, ng))) return rc;
         if ((rc = ensure(c, c->blk, (size_t)P * PFAAI_NTETRAMERS * sizeof(uint4)))) return rc;
     }
@@ -1157,7 +1199,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
             fp16_done = true;
             c->load_path = PFAAI_LOAD_F_FROM_G;
             if (want_pos && ng < ((int64_t)1 << 32)) {  // the WK 3 walks' G_pos and G_end
-                if (!(c->G_end.p) && (rc = ensure(c, c->G_end, n_f * sizeof(uint32_t)))) return rc;
+                if (!(c->G_pe.p) && (rc = ensure(c, c->G_pe, n_f * sizeof(uint2)))) return rc;
                 rc = build_gpos_ends(c, n_f, g_lo, g_hi, gbase, n_kept, nullptr, s);
                 ends_built = rc == PFAAI_RC_OK;
                 if (rc == -1 && (rc = build_gpos_from_f(c, n_f, s))) return rc;  // (G_end from k_gend below)
@@ -1279,7 +1321,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
     d.tcol_col = static_cast<const int32_t*>(c->tcol_col.p);
     d.G_off = has_g ? static_cast<const int64_t*>(c->G_off.p) : nullptr;
     d.G_tet = has_g ? static_cast<const int32_t*>(c->G_tet.p) : nullptr;
-    d.G_pos = c->G_pos.p ? static_cast<const uint32_t*>(c->G_pos.p) : nullptr;
+    const bool have_pos = c->G_pos.p != nullptr;
     d.blk = has_g ? static_cast<uint4*>(c->blk.p) : nullptr;
     d.Fp16 = static_cast<const uint16_t*>(c->Fp16.p);
     d.T16 = static_cast<const uint16_t*>(c->T16.p);
@@ -1289,15 +1331,17 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
     // up once here (k_blk_end + k_gend).  The WK 3 row kernel then reads
     // (G_pos, G_end) of its G entries with coalesced loads instead of one
     // run-table lookup per entry and step, and its steps build no run table.
-    d.G_end = nullptr;
+    d.G_pe = nullptr;
     c->runs_valid = false;
     {
         // k_gend: G_end (with G_pos) and / or the G sides of the both-given check
         const int ggrid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(ng, kGendLists), 1), 1 << 16);
         auto* sums = static_cast<unsigned long long*>(c->scalars.p) + SC_HG;
-        if (d.G_pos && ends_built) {  // G_end came with G_pos; the G side of the check ran beside the sort
-            d.G_end = static_cast<const uint32_t*>(c->G_end.p);
-        } else if (d.G_pos) {
+        if (have_pos && ends_built) {  // G_pe came from the run-end sort; the G side of the check ran beside it
+            d.G_pe = static_cast<const uint2*>(c->G_pe.p);
+            release(c->G_pos);  // (not written on this path)
+            release(c->G_end);
+        } else if (have_pos) {
             if ((rc = ensure(c, c->G_end, std::max<int64_t>(n_f, 1) * sizeof(uint32_t)))) return rc;
             if ((rc = build_runs_g<0>(c, s, false, true))) return rc;  // the u32 run-end table, into blk
             const auto* ends = reinterpret_cast<const uint32_t*>(c->blk.p);
@@ -1309,9 +1353,14 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
                 hipLaunchKernelGGL((k_gend<true, false>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P, ends,
                                    gend, 0ull, 0ull, nullptr, 0, ni);
             HIPCHK(c, hipGetLastError());
-            d.G_end = static_cast<const uint32_t*>(c->G_end.p);
+            if ((rc = ensure(c, c->G_pe, std::max<int64_t>(n_f, 1) * sizeof(uint2)))) return rc;
+            hipLaunchKernelGGL(k_pack_pe, dim3((int)std::min<int64_t>(ceil_div(n_f, 256), 1 << 16)), dim3(256), 0, s,
+                               static_cast<const uint32_t*>(c->G_pos.p), gend, n_f, static_cast<uint2*>(c->G_pe.p));
+            HIPCHK(c, hipGetLastError());
+            d.G_pe = static_cast<const uint2*>(c->G_pe.p);
         } else {
             release(c->G_end);
+            release(c->G_pe);
             if (g_check) {
                 hipLaunchKernelGGL((k_gend<false, true>), dim3(ggrid), dim3(256), 0, s, d.G_off, d.G_tet, ng, P,
                                    nullptr, nullptr, check_seed, check_seed2, sums, 0, ni);
@@ -1321,7 +1370,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
         // member codes for the WK 3 walks (all-vs-all with G_pos / G_end):
         // the run-end sort's histogram pass wrote them; else k_fcode
         d.Fcode = nullptr;
-        if (d.G_end && p.mode == PFAAI_MODE_ALL) {
+        if (d.G_pe && p.mode == PFAAI_MODE_ALL) {
             if (!ends_built) {
                 if ((rc = ensure(c, c->Fcode, (size_t)(n_f + 16) * sizeof(uint32_t)))) return rc;
                 hipLaunchKernelGGL(k_fcode, dim3((int)std::min<int64_t>(ceil_div(n_f + 16, 256), 1 << 16)), dim3(256), 0,
@@ -1423,6 +1472,9 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
         preload_rows<2>();
         preload_rows<kModeFull>();
     }
+    if (hipHostMalloc(&c->d2h_host, 2 * kD2hChunk, hipHostMallocDefault) != hipSuccess) c->d2h_host = nullptr;
+    for (hipEvent_t& e : c->d2h_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
     *out = c;
     return PFAAI_RC_OK;
 }
@@ -1432,7 +1484,7 @@ int pfaai_destroy(pfaai_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&c->T16, &c->T16c, &c->Fp16, &c->Lp, &c->Fp, &c->Fg, &c->T, &c->is_q, &c->q_index, &c->t_rank, &c->row_of,
-                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->Fcode, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
+                      &c->row_genome, &c->tcol_row, &c->tcol_col, &c->G_off, &c->G_tet, &c->G_pos, &c->G_end, &c->G_pe, &c->Fcode, &c->blk, &c->rowptr, &c->lens, &c->cnt_t, &c->off_t, &c->key_c, &c->rec_c, &c->key_a,
                       &c->key_b, &c->val_a, &c->val_b, &c->hist, &c->hoff, &c->recs, &c->sums, &c->scalars,
                       &c->out_aji, &c->out_S, &c->out_N, &c->dbg, &c->blkw, &c->srec_a, &c->srec_b, &c->shist,
                       &c->sgsum, &c->sbase, &c->tails, &c->ranks})
@@ -1446,6 +1498,9 @@ int pfaai_destroy(pfaai_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     release(c->st_dev);
     if (c->st_host) (void)hipHostFree(c->st_host);
+    if (c->d2h_host) (void)hipHostFree(c->d2h_host);
+    for (hipEvent_t e : c->d2h_ev)
+        if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
         if (c->st_done[i]) (void)hipEventDestroy(c->st_done[i]);
         if (c->st_copied[i]) (void)hipEventDestroy(c->st_copied[i]);
@@ -1558,7 +1613,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // launch would leave the column windows for whole-run walks pruned by
     // three splitters (100k streamed: 613 -> 689 ms).  PFAAI_PL_LAUNCH_COLS=0
     // keeps the problem's widest row (A/B; results identical)
-    if (!full && c->prob.mode == PFAAI_MODE_ALL && c->dev.G_pos) {
+    if (!full && c->prob.mode == PFAAI_MODE_ALL && c->dev.G_pe) {
         const char* lc = DIAG_ENV("PFAAI_PL_LAUNCH_COLS");
         if (!(lc && lc[0] == '0')) c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - rb);
     }
@@ -1588,9 +1643,9 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     HIPCHK(c, hipMemsetAsync(N, 0, np * sizeof(int32_t), c->stream));
     rc = pfaai_run(c, 0, c->n_rows, flags | PFAAI_FLAG_EMIT_JAC, aji, S, N, c->stream);
     if (rc) return rc;
-    if (h_aji) HIPCHK(c, hipMemcpyAsync(h_aji, aji, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (h_S) HIPCHK(c, hipMemcpyAsync(h_S, S, np * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (h_N) HIPCHK(c, hipMemcpyAsync(h_N, N, np * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (h_aji && (rc = d2h_staged(c, h_aji, aji, np * sizeof(double), c->stream))) return rc;
+    if (h_S && (rc = d2h_staged(c, h_S, S, np * sizeof(double), c->stream))) return rc;
+    if (h_N && (rc = d2h_staged(c, h_N, N, np * sizeof(int32_t), c->stream))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PFAAI_RC_OK;
 }
@@ -1716,6 +1771,19 @@ __global__ void k_div_check(int32_t c_max, int32_t d_max, unsigned long long* ba
         const double q0 = (double)c / (double)d;
         const double q1 = exact_div_small<NS>((double)c, (double)d);
         nb += __double_as_longlong(q0) != __double_as_longlong(q1);
+        // k_rows_pl's paired form (exact_div_pair: one reciprocal of d * d1
+        // for both columns of a counter word) against partners d1 across
+        // the range, both columns checked
+        const int32_t d1s[6] = {1, (int32_t)d, (int32_t)d + 1, 2 * (int32_t)d - 1,
+                                (int32_t)((d * 7919) % 131071) + 1, 131071};
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            const int32_t d1 = d1s[u], c1 = (int32_t)min<int64_t>(c, d1);
+            double s0 = 0.0, s1 = 0.0;
+            exact_div_pair(c, (int32_t)d, c1, d1, s0, s1);
+            nb += (__double_as_longlong(s0) != __double_as_longlong(q0)) +
+                  (__double_as_longlong(s1) != __double_as_longlong((double)c1 / (double)d1));
+        }
     }
     if (nb) atomicAdd(bad, nb);
     (void)c_max;
@@ -2128,9 +2196,9 @@ int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, dou
     }
     rc = pfaai_run(c, rb, re, flags | PFAAI_FLAG_EMIT_JAC, aji - f, S - f, N - f, c->stream);
     if (rc) return rc;
-    if (h_aji) HIPCHK(c, hipMemcpyAsync(h_aji + f, aji, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (h_S) HIPCHK(c, hipMemcpyAsync(h_S + f, S, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    if (h_N) HIPCHK(c, hipMemcpyAsync(h_N + f, N, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (h_aji && (rc = d2h_staged(c, h_aji + f, aji, n * sizeof(double), c->stream))) return rc;
+    if (h_S && (rc = d2h_staged(c, h_S + f, S, n * sizeof(double), c->stream))) return rc;
+    if (h_N && (rc = d2h_staged(c, h_N + f, N, n * sizeof(int32_t), c->stream))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PFAAI_RC_OK;
 }

@@ -60,8 +60,8 @@ struct Dev {
     const int32_t* tcol_col;    // [n_ids] T column used when the genome is genomeB
     const int64_t* G_off;       // [n_ids * n_prot + 1] genome-major CSR (optional)
     const int32_t* G_tet;
-    const uint32_t* G_pos;      // [|G|] F index of each G entry (all-vs-all; nullptr if not built)
-    const uint32_t* G_end;      // [|G|] end of the F run of each G entry (built with G_pos)
+    const uint2* G_pe;          // [|G|] (F index, end of its F run) of each G entry: the all-vs-all
+                                // walk data (G_pos, G_end interleaved; nullptr if not built)
     const uint32_t* Fcode;      // [|F| + 16] member codes of F for the WK 3 walks (k_fcode), or nullptr
     uint4* blk;                 // [n_prot * 160000] (protein, tetramer) -> F run, see k_blk
     const uint16_t* Fp16;       // [|F|] protein of each F entry, u16 (k_blk)

@@ -9,7 +9,7 @@
 namespace pfaai_impl {
 
 // k_rows_pl's variant bits for the WK 3 walks (pfaai_rows_pl.hpp V): the
-// release form kPlV; PFAAI_PL_V=0, 3, 19, 25 overrides it (diagnostics, A/B).
+// release form kPlV; PFAAI_PL_V=0 selects round 4's form (diagnostics, A/B).
 // The other forms (column windows, -q, -r, full rows) take kPlVG's S5 bits
 // where they do not spill (MODE 2 compiles both S5 forms: 114 VGPRs spilled,
 // so -r keeps V 0); PFAAI_PL_VG=0 overrides (A/B).
@@ -51,14 +51,9 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
                 if (gp) {  // (G_pos is built up to 20 480 genomes only: never BIGF)
                     if (bigf) { PLK(true, 3, 0); return; }
 #ifdef PFAAI_DIAGNOSTICS
-                    if (const char* v = DIAG_ENV("PFAAI_PL_V")) {
-                        switch (atoi(v)) {
-                            case 0: PLK(false, 3, 0); return;
-                            case 3: PLK(false, 3, 3); return;
-                            case 19: PLK(false, 3, 19); return;
-                            case 25: PLK(false, 3, 25); return;
-                            default: break;
-                        }
+                    if (const char* v = DIAG_ENV("PFAAI_PL_V"); v && atoi(v) == 0) {  // round 4's form (A/B)
+                        PLK(false, 3, 0);
+                        return;
                     }
 #endif
                     PLK(false, 3, kPlV);

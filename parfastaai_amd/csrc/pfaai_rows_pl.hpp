@@ -301,14 +301,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // the 1024 entries: 11 of 16 waves are idle), so it skips them -- a
     // wave-uniform branch (10.17 -> 9.96 ms at 10k)
     const uint32_t wbase0 = uni_u32((uint32_t)tid & ~63u);
-    // WK 3: S1 loads each entry's G_pos and G_end (the end of its F run,
-    // built at load) -- two coalesced loads, no tetramer id and no run-table
-    // lookup; S2 only carries them on (gq -> gq2, gt -> r4.y); S3 cuts
-    // [G_pos + 1, G_end) into 16-member tasks from an 8-aligned start
-    // (pl_issue_m2<A8>)
+    // WK 3: S1 loads each entry's (G_pos, G_end) (the end of its F run,
+    // built at load; one 8-B load from the interleaved G_pe) -- no tetramer
+    // id and no run-table lookup; S3 cuts [G_pos + 1, G_end) into 16-member
+    // tasks from an 8-aligned start (pl_issue_m2<A8>)
     constexpr bool GP = WK == 3;
-    const rsrc_t r_gp = mk_rsrc(GP ? d.G_pos + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
-    const rsrc_t r_ge = mk_rsrc(GP ? d.G_end + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 4u : 0u);
+    const rsrc_t r_gpe = mk_rsrc(GP ? d.G_pe + g0 : nullptr, GP ? (uint64_t)uni_u32(goff[P]) * 8u : 0u);
     // WK 3: S1's loads are issued by every wave (out-of-range offsets read
     // 0): a load issued under the wave skip made the number of loads in
     // flight path-dependent, and the compiler then waited for everything
@@ -324,8 +322,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         for (int j = 0; j < EPT; ++j) {
             const uint32_t e = (uint32_t)(tid + j * NT);
             if constexpr (GP) {
-                gq[j] = bld_u32(r_gp, e < n ? e * 4u : kOOB, o * 4u);
-                gt[j] = (int32_t)bld_u32(r_ge, e < n ? e * 4u : kOOB, o * 4u);  // run end (0 past the list)
+                const uint2 pe = bld_u64(r_gpe, e < n ? e * 8u : kOOB, o * 8u);  // (0, 0) past the list
+                gq[j] = pe.x;
+                gt[j] = (int32_t)pe.y;  // run end
             } else {
                 gt[j] = (int32_t)bld_u32(r_g, e < n ? e * 4u : kOOB, o * 4u);
             }

@@ -612,10 +612,12 @@ struct DstRecsEnds {
     }
 };
 
-// pass 2 (G order): G_pos = the F index, G_end = its run end
+// pass 2 (G order): G_pe = (the F index, its run end), one 8-B store per
+// entry -- a tile's digit run is one contiguous 32-B piece of one array
+// instead of two 16-B pieces of G_pos and G_end (2.06 ms for the pass at 10k
+// with the two arrays)
 struct DstGposEnds {
-    uint32_t* G_pos;
-    uint32_t* G_end;
+    uint2* G_pe;
     int hb;
     static constexpr int kWH = kSortItems;
     static constexpr bool kSum = false;
@@ -623,8 +625,7 @@ struct DstGposEnds {
     __device__ __forceinline__ Aux fetch(int64_t, uint64_t) const { return {}; }
     __device__ __forceinline__ uint64_t store(int64_t pos, uint64_t v, Aux, int64_t) const {
         const uint32_t i = (uint32_t)(v >> hb), dist = (uint32_t)(v >> (hb + 32));
-        G_pos[pos] = i;
-        G_end[pos] = i + dist;
+        G_pe[pos] = make_uint2(i, i + dist);
         return 0;
     }
 };

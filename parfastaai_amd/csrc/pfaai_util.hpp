@@ -18,6 +18,10 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint64_t bytes) {
 __device__ __forceinline__ uint32_t bld_u32(rsrc_t r, uint32_t voff, uint32_t soff) {
     return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
 }
+__device__ __forceinline__ uint2 bld_u64(rsrc_t r, uint32_t voff, uint32_t soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    return make_uint2((uint32_t)v[0], (uint32_t)v[1]);
+}
 __device__ __forceinline__ uint4 bld_u128(rsrc_t r, uint32_t voff, uint32_t soff) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
     return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);

@@ -3,8 +3,12 @@
 // They expose exactly the accessors pfaai::ParFAAIHipImpl (include/
 // pfaai_hip.hpp) and printOutput need, with the reference's names.
 #pragma once
+#include <sys/mman.h>
+
+#include <algorithm>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -16,7 +20,28 @@ struct JACTuple {  // JACTuple<int, double>, interface.hpp:61-75
     int32_t genomeA, genomeB;
     double S;
     int32_t N;
+    // no zero-fill on construction: initJAC writes every field, in parallel
+    // (a vector of n value-initialised tuples is a serial 24n-byte memset)
+    JACTuple() {}
+    JACTuple(int32_t a, int32_t b, double s, int32_t n) : genomeA(a), genomeB(b), S(s), N(n) {}
 };
+
+// transparent huge pages for an untouched allocation (see pfaai::detail::advise_huge)
+inline void advise_huge(const void* p, std::size_t bytes) {
+    const auto a = (reinterpret_cast<std::uintptr_t>(p) + (((std::uintptr_t)1 << 21) - 1)) & ~(((std::uintptr_t)1 << 21) - 1);
+    const auto e = reinterpret_cast<std::uintptr_t>(p) + bytes;
+    if (e > a + ((std::uintptr_t)1 << 21)) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+}
+
+// fn(lo, hi) over [0, n) on up to 8 threads (>= 64k items each)
+template <class Fn>
+void par_items(int64_t n, Fn fn) {
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
+    fn(0, n / nt);
+    for (auto& x : th) x.join();
+}
 
 class DataBase {
   public:
@@ -58,16 +83,26 @@ class AllData : public DataBase {
     bool isQryGenome(int32_t) const { return true; }
     int32_t mapQueryId(int32_t g) const { return g; }
     int32_t mapTargetId(int32_t g) const { return g; }
+    // pair k of row a (columns a+1..n-1) sits at n a - a (a + 1) / 2 + b - a - 1
+    // (ds_impl.hpp:83-86); each thread finds its first pair's row by
+    // bisection and walks on
     std::vector<JACType> initJAC() const {
         std::vector<JACType> j(nGenomePairs());
-        int32_t a = 0, b = 1;
-        for (auto& x : j) {
-            x.genomeA = a;
-            x.genomeB = b;
-            x.S = 0.0;
-            x.N = 0;
-            if (b == n() - 1) { ++a; b = a + 1; } else { ++b; }
-        }
+        advise_huge(j.data(), j.size() * sizeof(JACType));
+        const int64_t nn = n();
+        auto first = [nn](int64_t a) { return nn * a - a * (a + 1) / 2; };
+        par_items((int64_t)j.size(), [&](int64_t lo, int64_t hi) {
+            int64_t a0 = 0, a1 = nn - 1;  // the row holding pair lo: first(a) <= lo < first(a + 1)
+            while (a0 < a1) {
+                const int64_t m = (a0 + a1 + 1) / 2;
+                if (first(m) <= lo) a0 = m; else a1 = m - 1;
+            }
+            int32_t a = (int32_t)a0, b = (int32_t)(a0 + 1 + lo - first(a0));
+            for (int64_t k = lo; k < hi; ++k) {
+                j[k] = JACType{a, b, 0.0, 0};
+                if (b == nn - 1) { ++a; b = a + 1; } else { ++b; }
+            }
+        });
         return j;
     }
 };
@@ -107,10 +142,12 @@ class QSubData : public DataBase {
     std::vector<JACType> initJAC() const {
         std::vector<JACType> j(nGenomePairs(), JACType{0, 0, 0.0, 0});
         const int64_t qt = qrySetSize() * nTgt();
-        for (int64_t i = 0; i < qt; ++i) {
-            j[i].genomeA = m_qlook[i / nTgt()];
-            j[i].genomeB = m_tlook[i % nTgt()];
-        }
+        par_items(qt, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; ++i) {
+                j[i].genomeA = m_qlook[i / nTgt()];
+                j[i].genomeB = m_tlook[i % nTgt()];
+            }
+        });
         int32_t a = 0, b = 1;
         for (int64_t i = qt; i < (int64_t)j.size(); ++i) {
             j[i].genomeA = m_qlook[a];
@@ -141,11 +178,12 @@ class QTData : public DataBase {
     int32_t mapTargetId(int32_t g) const { return mapQueryId(g); }
     // the reference's ids (i/nT, nQ + i%nT), ds_impl.hpp:434-436
     std::vector<JACType> initJAC() const {
-        std::vector<JACType> j(nGenomePairs(), JACType{0, 0, 0.0, 0});
-        for (int64_t i = 0; i < (int64_t)j.size(); ++i) {
-            j[i].genomeA = (int32_t)(i / tgtSetSize());
-            j[i].genomeB = (int32_t)(qrySetSize() + i % tgtSetSize());
-        }
+        std::vector<JACType> j(nGenomePairs());
+        advise_huge(j.data(), j.size() * sizeof(JACType));
+        const int64_t nT = tgtSetSize(), nQ = qrySetSize();
+        par_items((int64_t)j.size(), [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; ++i) j[i] = JACType{(int32_t)(i / nT), (int32_t)(nQ + i % nT), 0.0, 0};
+        });
         return j;
     }
 };

@@ -376,9 +376,10 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         pfaai_load_timing(impl.context(), &lc, &lu, &ld);
         const double ms_ctor = std::chrono::duration<double, std::milli>(t1 - t0).count();
         std::printf("  breakdown         : context %.1f + load checks %.1f, H2D %.1f, device F/G %.1f ms; run %.1f ms = "
-                    "run tables %.2f + %s %.2f + D2H / JAC fill %.1f ms\n",
+                    "run tables %.2f + %s %.2f + D2H / JAC fill %.1f ms\n"
+                    "  host side of run  : engine compute + D2H done at %.1f, initJAC (beside it) at %.1f, JAC fill %.1f ms\n",
                     ms_ctor - lc - lu - ld, lc, lu, ld, ms_run, impl.msBuild(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?",
-                    impl.msRows(), ms_run - impl.msBuild() - impl.msRows());
+                    impl.msRows(), ms_run - impl.msBuild() - impl.msRows(), impl.msCompute(), impl.msIds(), impl.msFill());
         if (app.pathToOutputFile.empty()) return 0;
         t1 = std::chrono::steady_clock::now();
         std::printf("Writing output with %lld query genomes and %lld target genomes. \n",

@@ -5,9 +5,16 @@ GPU, copied to pinned host memory while the next tile computes
 (pfaai_stream), and copied by the sink into one host array of the whole
 JAC-ordered output (N = 100 000: 5e9 pairs, 40 GB).  Prints one JSON line:
 pairs/s end to end (device compute + D2H + host copy, inputs resident),
-|E|, tiles, and the device-side k_rows time.
+|E|, tiles, and the device-side k_rows time.  The stream runs once per
+--sinks entry on the same load, so the parts of the wall separate:
+  noop   the sink returns at once: device compute + D2H into the pinned tile
+         buffers (the library's side alone)
+  copy   one numpy copy of each tile into the output array (round 4's sink)
+  par    the same copy cut into --threads slices on a thread pool (numpy
+         releases the GIL while it copies)
+The wall of the last sink is the line's wall_s.
 
-    python tools/gpu/stream_bench.py --genomes 100000 --tile-pairs 268435456
+    python tools/gpu/stream_bench.py --genomes 100000 --tile-pairs 268435456 --sinks noop copy par
 """
 import argparse
 import json
@@ -32,7 +39,10 @@ def main():
     ap.add_argument("--prot", type=int, default=100)
     ap.add_argument("--tile-pairs", type=int, default=1 << 28)
     ap.add_argument("--check-rows", type=int, default=2, help="rows re-checked against a pfaai_run of them")
+    ap.add_argument("--sinks", nargs="+", default=["par"], choices=["noop", "copy", "par"])
+    ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
+    from concurrent.futures import ThreadPoolExecutor
     from parfastaai_amd import _capi, syn
 
     t0 = time.perf_counter()
@@ -47,25 +57,38 @@ def main():
     log(f"pfaai_load {time.perf_counter() - t0:.1f}s")
     n_rows, n_pairs = eng.shape()
     out = np.empty(n_pairs, dtype=np.float64)
-    out[:: 1 << 16] = 0.0  # touch
+    out[:: 1 << 9] = 0.0  # touch every 4-KB page: the walls measure copies, not first-touch faults
     tiles = [0]
     last = [time.perf_counter()]
+    pool = ThreadPoolExecutor(max_workers=args.threads)
 
-    def sink(rb, re, first, aji, S, N):
-        out[first: first + len(aji)] = aji
-        tiles[0] += 1
-        now = time.perf_counter()
-        if now - last[0] > 20:
-            log(f"tile {tiles[0]}: rows [{rb}, {re})")
-            last[0] = now
-        return 0
+    def sink(kind):
+        def fn(rb, re, first, aji, S, N):
+            if kind == "copy":
+                out[first: first + len(aji)] = aji
+            elif kind == "par":
+                n, k = len(aji), args.threads
+                cuts = [n * i // k for i in range(k + 1)]
+                list(pool.map(lambda i: out.__setitem__(slice(first + cuts[i], first + cuts[i + 1]),
+                                                        aji[cuts[i]: cuts[i + 1]]), range(k)))
+            tiles[0] += 1
+            now = time.perf_counter()
+            if now - last[0] > 20:
+                log(f"tile {tiles[0]}: rows [{rb}, {re})")
+                last[0] = now
+            return 0
+        return fn
 
-    eng.timing(reset=True)
-    t0 = time.perf_counter()
-    n_events = eng.stream(0, n_rows, args.tile_pairs, 0, sink)
-    wall = time.perf_counter() - t0
-    n_runs, ms_build, ms_rows = eng.timing(reset=True)
-    log(f"streamed {tiles[0]} tiles in {wall:.2f}s")
+    walls = {}
+    for kind in args.sinks:
+        tiles[0] = 0
+        eng.timing(reset=True)
+        t0 = time.perf_counter()
+        n_events = eng.stream(0, n_rows, args.tile_pairs, 0, sink(kind))
+        walls[kind] = round(time.perf_counter() - t0, 3)
+        n_runs, ms_build, ms_rows = eng.timing(reset=True)
+        log(f"sink {kind}: streamed {tiles[0]} tiles in {walls[kind]:.2f}s")
+    wall = walls[args.sinks[-1]]
     # spot check: a few rows recomputed with pfaai_run into device memory
     ok = True
     for r in np.linspace(0, n_rows - 2, args.check_rows).astype(int):
@@ -79,7 +102,8 @@ def main():
         "what": "pfaai_stream all-vs-all, AJI tiles to host (SURVEY 8f rank 4, config C5 shape on 1 GPU)",
         "genomes": args.genomes, "proteins": args.prot, "F": n_f, "pairs": n_pairs, "events": n_events,
         "tiles": tiles[0], "tile_pairs": args.tile_pairs,
-        "wall_s": round(wall, 3), "pairs_per_s": round(n_pairs / wall, 1),
+        "wall_s": round(wall, 3), "pairs_per_s": round(n_pairs / wall, 1), "walls_by_sink_s": walls,
+        "sink_threads": args.threads,
         "device_ms_rows": round(ms_rows, 2), "device_ms_build": round(ms_build, 2), "runs": n_runs,
         "device_pairs_per_s": round(n_pairs / (ms_rows + ms_build) * 1e3, 1),
         "d2h_GBps_effective": round(8 * n_pairs / wall / 1e9, 2),
