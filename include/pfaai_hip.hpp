@@ -35,6 +35,7 @@
 #include <cstdio>
 #include <exception>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <system_error>
@@ -68,14 +69,34 @@ struct CtxDeleter {
 };
 using CtxPtr = std::unique_ptr<pfaai_ctx, CtxDeleter>;
 
+// Contexts created ahead of the engine (prewarm_context) wait here for the
+// first make_ctx of their device.
+struct Parked {
+    std::mutex mu;
+    std::vector<std::pair<int, pfaai_ctx*>> ctx;
+};
+inline Parked& parked() {
+    static Parked p;
+    return p;
+}
+
 inline CtxPtr make_ctx(int device) {
+    {
+        Parked& pk = parked();
+        std::lock_guard<std::mutex> lk(pk.mu);
+        for (auto it = pk.ctx.begin(); it != pk.ctx.end(); ++it)
+            if (it->first == device) {
+                pfaai_ctx* c = it->second;
+                pk.ctx.erase(it);
+                return CtxPtr(c);
+            }
+    }
     pfaai_ctx* c = nullptr;
     const int rc = pfaai_create(&c, device);
     if (rc) throw HipError(rc, "pfaai_create failed for device " + std::to_string(device) + " (no visible MI355X?)");
     return CtxPtr(c);
 }
 
-// [0, n) over up to 16 host threads (the adapter's array conversions)
 // Ask for transparent huge pages on a large allocation nothing has touched
 // yet: its first touch then faults 2-MB pages instead of 4-KB ones (the
 // CLI's C2 output arrays, 64 MB, took ~15 ms of page faults at 4 KB,
@@ -87,6 +108,7 @@ inline void advise_huge(const void* p, std::size_t bytes) {
     if (e > a + ((std::uintptr_t)1 << 21)) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
 }
 
+// [0, n) over up to 16 host threads (the adapter's array conversions)
 template <class Fn>
 void par_range(int64_t n, Fn fn) {
     // >= 64k elements per thread (a 2M-pair JAC fill ran on one thread at the
@@ -103,6 +125,20 @@ void par_range(int64_t n, Fn fn) {
     for (auto& x : th) x.join();
 }
 }  // namespace detail
+
+// Create device `device`'s context now (the HIP runtime's first
+// initialisation, streams, pinned staging, code objects: ~100 ms on a fresh
+// process) and keep it for the next engine constructed on that device.  The
+// CLI calls it on a helper thread while it reads SQLite.  Thread-safe; false
+// if the context could not be created (the engine then reports why).
+inline bool prewarm_context(int device) {
+    pfaai_ctx* c = nullptr;
+    if (pfaai_create(&c, device) != PFAAI_RC_OK) return false;
+    detail::Parked& pk = detail::parked();
+    std::lock_guard<std::mutex> lk(pk.mu);
+    pk.ctx.emplace_back(device, c);
+    return true;
+}
 
 // Contiguous row blocks over `parts` devices: cut[0] = 0 .. cut[parts] = n,
 // balanced by the row-cost model of parfastaai_amd/shard.py:split_rows (the
@@ -212,6 +248,25 @@ class ParFAAIHipImpl {
     ParFAAIHipImpl(const DSIT& ds, int mode, const std::vector<int>& devices, bool ref_compat = false)
         : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
         if (devices.empty()) throw HipError(PFAAI_RC_INVALID, "no device");
+        // computeJAC's host side -- initJAC and the first touch of the output
+        // arrays -- on a helper thread while the contexts are made and the
+        // problem uploads, when the outputs are small enough (<= kPrepPairs)
+        // that holding them from construction costs little: the CLI's C2
+        // run phase was 21 ms of page faults and initJAC beside 1.6 ms of
+        // device work (round 5)
+        const int64_t np = (int64_t)ds.nGenomePairs();
+        if (np > 0 && np <= kPrepPairs) {
+            try {
+                m_prep.t = std::thread([this] {
+                    try {
+                        prepare_outputs();
+                    } catch (...) {
+                        m_prepErr = std::current_exception();
+                    }
+                });
+            } catch (const std::system_error&) {  // no thread: computeJAC prepares them itself
+            }
+        }
         // contexts are owned by RAII handles: a throw below releases them
         m_ctx.push_back(detail::make_ctx(devices[0]));
         for (std::size_t i = 1; i < devices.size() && mode != PFAAI_MODE_QSUB; ++i)
@@ -232,31 +287,37 @@ class ParFAAIHipImpl {
         int64_t rows = 0, pairs = 0;
         pfaai_shape(ctx(), &rows, &pairs);
         const std::size_t n = (std::size_t)pairs;
-        std::unique_ptr<double[]> S(new double[n ? n : 1]);  // no value-initialisation: the device fills them
-        std::unique_ptr<int32_t[]> N(new int32_t[n ? n : 1]);
-        detail::advise_huge(S.get(), n * sizeof(double));
-        detail::advise_huge(N.get(), n * sizeof(int32_t));
-        m_AJIdev.clear();
-        m_AJIdev.shrink_to_fit();
-        m_AJIdev.reserve(n);  // (untouched: huge pages before the zero fill)
-        detail::advise_huge(m_AJIdev.data(), n * sizeof(double));
-        m_AJIdev.resize(n);
+        join_prep();
+        m_prepAhead = m_prepared && m_S && m_JAC.size() == n && m_AJIdev.size() == n;
+        std::unique_ptr<double[]> S;
+        std::unique_ptr<int32_t[]> N;
+        if (m_prepAhead) {
+            S = std::move(m_S);
+            N = std::move(m_N);
+        } else {
+            alloc_outputs(n, S, N);
+        }
+        m_prepared = false;
+        m_S.reset();
+        m_N.reset();
         const uint32_t flags = m_compat ? PFAAI_FLAG_REF_COMPAT : 0u;
         std::thread ids;
-        bool ids_async = true;
+        bool ids_async = !m_prepAhead;
         std::exception_ptr ids_err;  // initJAC's exception, rethrown on this thread
-        try {
-            ids = std::thread([this, &ids_err, t0, ms_since] {
-                try {
-                    m_JAC = m_ds.initJAC();
-                    m_msIds = ms_since(t0);
-                } catch (...) {
-                    ids_err = std::current_exception();
-                }
-            });
-        } catch (const std::system_error&) {
-            ids_async = false;
-            m_JAC = m_ds.initJAC();
+        if (!m_prepAhead) {
+            try {
+                ids = std::thread([this, &ids_err, t0, ms_since] {
+                    try {
+                        m_JAC = m_ds.initJAC();
+                        m_msIds = ms_since(t0);
+                    } catch (...) {
+                        ids_err = std::current_exception();
+                    }
+                });
+            } catch (const std::system_error&) {
+                ids_async = false;
+                m_JAC = m_ds.initJAC();
+            }
         }
         int rc = PFAAI_RC_OK;
         std::string err;
@@ -299,7 +360,8 @@ class ParFAAIHipImpl {
     }
     // algorithm_impl.hpp:309-322 (the kernel epilogue already divided S / N)
     int computeAJI() {
-        if (m_AJIdev.size() != m_JAC.size() || m_JAC.empty()) {
+        join_prep();
+        if (m_prepared || m_AJIdev.size() != m_JAC.size() || m_JAC.empty()) {
             if (!m_JAC.empty() && m_AJI.size() == m_JAC.size()) return 0;  // already moved out
             computeJAC();
         }
@@ -323,6 +385,7 @@ class ParFAAIHipImpl {
     // tile -- neither the host nor the device holds the whole output.  ALL and
     // QT modes.  Returns 0, or the engine / I/O error code.
     int streamAJI(const std::string& path, int64_t tile_pairs) {
+        drop_prepared();
         int64_t rows = 0, pairs = 0;
         int rc = pfaai_shape(ctx(), &rows, &pairs);
         if (rc) throw HipError(rc, pfaai_last_error(ctx()));
@@ -347,6 +410,7 @@ class ParFAAIHipImpl {
     // sink(user, row_begin, row_end, n_cols, block) -- the whole matrix is
     // never held.  Returns 0 or throws the engine error.
     int streamMatrix(int64_t tile_rows, pfaai_matrix_sink_fn sink, void* user) {
+        drop_prepared();
         int64_t rows = 0;
         int rc = pfaai_shape(ctx(), &rows, nullptr);
         if (!rc) rc = pfaai_stream_matrix(ctx(), 0, rows, tile_rows, m_compat ? PFAAI_FLAG_REF_COMPAT : 0u, sink, user);
@@ -370,6 +434,9 @@ class ParFAAIHipImpl {
     // done (on its thread), the engine's compute + D2H done; and the JAC
     // tuple fill after both
     float msIds() const { return m_msIds; }
+    // whether the last computeJAC found initJAC and its output pages made
+    // during construction (msIds is then that helper thread's own time)
+    bool preparedAhead() const { return m_prepAhead; }
     float msCompute() const { return m_msCompute; }
     float msFill() const { return m_msFill; }
     float msBuild() const { return m_msBuild; }
@@ -385,6 +452,56 @@ class ParFAAIHipImpl {
 
   private:
     pfaai_ctx* ctx() const { return m_ctx.front().get(); }
+
+    static constexpr int64_t kPrepPairs = (int64_t)1 << 26;  // 44 B a pair: <= 2.75 GiB of host outputs
+
+    // S / N (filled by the device, never value-initialised) and the AJI
+    // vector, asking for huge pages before their first touch
+    void alloc_outputs(std::size_t n, std::unique_ptr<double[]>& S, std::unique_ptr<int32_t[]>& N) {
+        S.reset(new double[n ? n : 1]);
+        N.reset(new int32_t[n ? n : 1]);
+        detail::advise_huge(S.get(), n * sizeof(double));
+        detail::advise_huge(N.get(), n * sizeof(int32_t));
+        m_AJIdev.clear();
+        m_AJIdev.shrink_to_fit();
+        m_AJIdev.reserve(n);  // (untouched: huge pages before the zero fill)
+        detail::advise_huge(m_AJIdev.data(), n * sizeof(double));
+        m_AJIdev.resize(n);
+    }
+    // the constructor's helper thread: initJAC, then the outputs allocated and
+    // every page of S / N touched (the device's D2H then lands in mapped pages)
+    void prepare_outputs() {
+        const auto t0 = std::chrono::steady_clock::now();
+        m_JAC = m_ds.initJAC();
+        const std::size_t n = m_JAC.size();
+        alloc_outputs(n, m_S, m_N);
+        double* S = m_S.get();
+        int32_t* N = m_N.get();
+        detail::par_range((int64_t)n, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi; i += 512) S[i] = 0.0;  // one store a 4 KB page
+            for (int64_t i = lo; i < hi; i += 1024) N[i] = 0;
+        });
+        m_msIds = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        m_prepared = true;
+    }
+    void join_prep() {
+        if (m_prep.t.joinable()) m_prep.t.join();
+        if (m_prepErr) {
+            std::exception_ptr e = m_prepErr;
+            m_prepErr = nullptr;
+            m_prepared = false;
+            std::rethrow_exception(e);
+        }
+    }
+    void drop_prepared() {
+        join_prep();
+        if (!m_prepared) return;
+        m_prepared = false;
+        m_S.reset();
+        m_N.reset();
+        std::vector<JACType>().swap(m_JAC);
+        std::vector<double>().swap(m_AJIdev);
+    }
 
     void computeMulti(uint32_t flags, double* S, int32_t* N) {
         int64_t rows = 0, pairs = 0;
@@ -500,6 +617,17 @@ class ParFAAIHipImpl {
     float m_msBuild = 0.f, m_msRows = 0.f;
     int32_t m_rowsKernel = -1;
     int32_t m_walk = PFAAI_WALK_NONE, m_narrow = 0;
+    // the constructor's output preparation (prepare_outputs)
+    std::unique_ptr<double[]> m_S;
+    std::unique_ptr<int32_t[]> m_N;
+    bool m_prepared = false, m_prepAhead = false;
+    std::exception_ptr m_prepErr;
+    struct Joiner {  // joined before the members above are destroyed (a throwing constructor included)
+        std::thread t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } m_prep;
 };
 
 }  // namespace pfaai

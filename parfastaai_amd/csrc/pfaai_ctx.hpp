@@ -38,6 +38,11 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// staged_copy's pinned buffer: kStageThreads host threads x two slots
+constexpr int kStageThreads = 16;
+constexpr size_t kStageSlot = (size_t)1 << 20;
+constexpr size_t kStageBytes = 2 * (size_t)kStageThreads * kStageSlot;
+
 }  // namespace pfaai_impl
 
 struct pfaai_ctx {
@@ -96,10 +101,10 @@ struct pfaai_ctx {
     hipEvent_t narrow_ev[2] = {nullptr, nullptr};
     std::vector<int64_t> row_fprefix;  // F entries of rows [0, r): exact work-list sizes
 
-    // staged D2H of host outputs (pfaai_compute / pfaai_compute_rows): two
-    // pinned chunks and their events (d2h_staged)
-    void* d2h_host = nullptr;
-    hipEvent_t d2h_ev[2] = {nullptr, nullptr};
+    // staged copies to / from the caller's pageable memory (staged_copy):
+    // kStageThreads pairs of kStageSlot-byte pinned slots and their events
+    void* stage_host = nullptr;
+    hipEvent_t stage_ev[2 * pfaai_impl::kStageThreads] = {};
     // output-tile streaming (pfaai_stream): copy stream, tile events, pinned buffers
     hipStream_t copy_stream = nullptr;
     hipEvent_t st_done[2] = {nullptr, nullptr}, st_copied[2] = {nullptr, nullptr};
@@ -194,10 +199,14 @@ inline void release(DevBuf& b) {
     b.bytes = 0;
 }
 
+// pfaai_hip.hip: pageable host <-> device through the context's pinned slots
+int staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t bytes, bool to_device, hipStream_t s);
+
 template <typename T>
 inline int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
     int rc = ensure(c, b, n * sizeof(T));
     if (rc) return rc;
+    if (n * sizeof(T) >= ((size_t)4 << 20)) return staged_copy(c, b.p, src, n * sizeof(T), true, c->stream);
     if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
     return PFAAI_RC_OK;
 }

@@ -6,6 +6,7 @@
 // F-only input, the sorted work lists, then the row kernel (K-S+J).
 
 #include <algorithm>
+#include <chrono>
 #include <random>
 #include <atomic>
 #include <thread>
@@ -53,48 +54,85 @@ int par_for(int64_t n, Fn fn, int64_t work = -1) {
 // exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
 
-// Device -> caller's host memory for the host-output entry points: chunks of
-// kD2hChunk bytes through two pinned buffers, the copy of chunk i overlapping
-// the host threads' memcpy of chunk i - 1 into dst.  A plain hipMemcpyAsync
-// into pageable memory that nothing has touched yet ran at ~2.5 GB/s (the
-// CLI's C2 outputs, 40 MB: 16 ms of its 18 ms pfaai_compute, round 5); the
-// pinned copies run at the link's rate and the page faults of dst are taken
-// by 16 threads at once.  Work ordered before on stream s is waited for.
-// The pinned pair is allocated by pfaai_create (a 64 MB hipHostMalloc at the
-// first compute cost the CLI's C2 run ~18 ms; at create it runs on the CLI's
-// helper thread beside the SQLite read).
-constexpr size_t kD2hChunk = (size_t)8 << 20;
-int d2h_staged(pfaai_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t s) {
+}  // namespace
+
+// Copies between the caller's pageable host memory and the device, both ways
+// (the host-output entry points' D2H, pfaai_load's large H2D uploads).  A
+// plain hipMemcpy to or from pageable memory runs through the runtime's own
+// staging on one thread: ~9 GB/s up (the CLI's C2 G_tet, 230 MB: 27 ms) and
+// ~2.5 GB/s down into memory nothing has touched yet (its 40 MB of outputs:
+// 16 ms), round 5.  Here up to kStageThreads host threads each own a
+// contiguous slice of the transfer and two kStageSlot-byte slots of the
+// context's pinned buffer (allocated by pfaai_create, so the CLI's helper
+// thread pays it beside the SQLite read): down, slot k's DMA is queued before
+// slot k - 1 is copied out to dst; up, slot k is filled from src while slot
+// k - 1's DMA runs.  The page faults of an untouched dst are taken by all
+// threads at once.  Work ordered before on stream s is waited for; on return
+// every byte has landed.
+int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t bytes, bool to_device, hipStream_t s) {
     if (bytes == 0) return PFAAI_RC_OK;
-    if (bytes < ((size_t)4 << 20)) {
-        HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    if (!c->stage_host && hipHostMalloc(&c->stage_host, kStageBytes, hipHostMallocDefault) != hipSuccess)
+        c->stage_host = nullptr;
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = (int)std::min<size_t>({(size_t)kStageThreads, (size_t)hw, bytes / (2 * kStageSlot)});
+    if (nt < 2 || !c->stage_host) {  // small (< 4 MB) or no pinned buffer: the runtime's own path
+        HIPCHK(c, hipMemcpyAsync(dst, src, bytes, to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         return PFAAI_RC_OK;
     }
-    if (!c->d2h_host) HIPCHK(c, hipHostMalloc(&c->d2h_host, 2 * kD2hChunk, hipHostMallocDefault));
-    for (hipEvent_t& e : c->d2h_ev)
-        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    const size_t nch = (bytes + kD2hChunk - 1) / kD2hChunk;
-    auto* h = static_cast<char*>(c->d2h_host);
-    auto host_copy = [&](size_t k) -> int {
-        const size_t off = k * kD2hChunk, len = std::min(kD2hChunk, bytes - off);
-        HIPCHK(c, hipEventSynchronize(c->d2h_ev[k & 1]));
-        char* d = static_cast<char*>(dst) + off;
-        const char* b = h + (k & 1) * kD2hChunk;
-        par_for((int64_t)len, [&](int64_t lo, int64_t hi, int) { std::memcpy(d + lo, b + lo, (size_t)(hi - lo)); });
-        return PFAAI_RC_OK;
-    };
-    for (size_t k = 0; k < nch; ++k) {
-        const size_t off = k * kD2hChunk, len = std::min(kD2hChunk, bytes - off);
-        HIPCHK(c, hipMemcpyAsync(h + (k & 1) * kD2hChunk, static_cast<const char*>(src) + off, len,
-                                 hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipEventRecord(c->d2h_ev[k & 1], s));
-        if (k >= 1) {  // chunk k - 1 to dst while chunk k is copied; buffer (k + 1) & 1 is then free
-            if (int rc = host_copy(k - 1)) return rc;
+    for (int i = 0; i < 2 * nt; ++i)
+        if (!c->stage_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+    std::vector<hipError_t> err((size_t)nt, hipSuccess);
+    auto slice = [&](int t) {
+        // [lo, hi) of the transfer, in slots of kStageSlot
+        const size_t lo = bytes * (size_t)t / (size_t)nt, hi = bytes * (size_t)(t + 1) / (size_t)nt;
+        char* pin[2] = {static_cast<char*>(c->stage_host) + (2 * (size_t)t) * kStageSlot,
+                        static_cast<char*>(c->stage_host) + (2 * (size_t)t + 1) * kStageSlot};
+        hipEvent_t ev[2] = {c->stage_ev[2 * t], c->stage_ev[2 * t + 1]};
+        const size_t ns = (hi - lo + kStageSlot - 1) / kStageSlot;
+        auto len = [&](size_t k) { return std::min(kStageSlot, hi - lo - k * kStageSlot); };
+        hipError_t e = hipSuccess;
+        if (to_device) {
+            for (size_t k = 0; k < ns && e == hipSuccess; ++k) {
+                if (k >= 2) e = hipEventSynchronize(ev[k & 1]);  // slot k & 1's previous DMA done
+                if (e != hipSuccess) break;
+                std::memcpy(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k));
+                e = hipMemcpyAsync(static_cast<char*>(dst) + lo + k * kStageSlot, pin[k & 1], len(k),
+                                   hipMemcpyHostToDevice, s);
+                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], s);
+            }
+            for (int j = 0; j < 2 && e == hipSuccess; ++j)
+                if ((size_t)j < ns) e = hipEventSynchronize(ev[j]);
+        } else {
+            auto out = [&](size_t k) -> hipError_t {
+                hipError_t r = hipEventSynchronize(ev[k & 1]);
+                if (r == hipSuccess) std::memcpy(static_cast<char*>(dst) + lo + k * kStageSlot, pin[k & 1], len(k));
+                return r;
+            };
+            for (size_t k = 0; k < ns && e == hipSuccess; ++k) {
+                e = hipMemcpyAsync(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k),
+                                   hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], s);
+                if (e == hipSuccess && k >= 1) e = out(k - 1);  // slot k - 1 out while slot k's DMA runs
+            }
+            if (e == hipSuccess) e = out(ns - 1);
         }
+        err[(size_t)t] = e;
+    };
+    std::vector<std::thread> th;
+    int started = 1;
+    try {
+        for (; started < nt; ++started) th.emplace_back(slice, started);
+    } catch (const std::system_error&) {
     }
-    return host_copy(nch - 1);
+    slice(0);
+    for (auto& x : th) x.join();
+    for (int t = started; t < nt; ++t) slice(t);  // threads that could not be started
+    for (hipError_t e : err) HIPCHK(c, e);
+    return PFAAI_RC_OK;
 }
+
+namespace {
 
 // Sort space for n keys: two key and two value ping-pong buffers, the
 // per-tile digit histograms and their scan (k_rs_hist / k_rs_scatter).
@@ -1472,9 +1510,19 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
         preload_rows<2>();
         preload_rows<kModeFull>();
     }
-    if (hipHostMalloc(&c->d2h_host, 2 * kD2hChunk, hipHostMallocDefault) != hipSuccess) c->d2h_host = nullptr;
-    for (hipEvent_t& e : c->d2h_ev)
+    if (hipHostMalloc(&c->stage_host, kStageBytes, hipHostMallocDefault) != hipSuccess) c->stage_host = nullptr;
+    for (hipEvent_t& e : c->stage_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    // one small copy each way through the pinned buffer: the first
+    // device-to-host copy of a process cost ~10 ms (the CLI's C2 AJI D2H:
+    // 11-20 ms for 16 MB, then 4 ms for the next 24 MB; round 5)
+    void* warm = nullptr;
+    if (c->stage_host && hipMalloc(&warm, kStageSlot) == hipSuccess) {  // a slot's size: the DMA engines' path
+        if (hipMemcpyAsync(warm, c->stage_host, kStageSlot, hipMemcpyHostToDevice, c->stream) == hipSuccess)
+            (void)hipMemcpyAsync(c->stage_host, warm, kStageSlot, hipMemcpyDeviceToHost, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(warm);
+    }
     *out = c;
     return PFAAI_RC_OK;
 }
@@ -1498,8 +1546,8 @@ int pfaai_destroy(pfaai_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     release(c->st_dev);
     if (c->st_host) (void)hipHostFree(c->st_host);
-    if (c->d2h_host) (void)hipHostFree(c->d2h_host);
-    for (hipEvent_t e : c->d2h_ev)
+    if (c->stage_host) (void)hipHostFree(c->stage_host);
+    for (hipEvent_t e : c->stage_ev)
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {
         if (c->st_done[i]) (void)hipEventDestroy(c->st_done[i]);
@@ -1632,6 +1680,8 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t np = c->n_pairs;
     int rc;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if ((rc = ensure(c, c->out_aji, np * sizeof(double)))) return rc;
     if ((rc = ensure(c, c->out_S, np * sizeof(double)))) return rc;
     if ((rc = ensure(c, c->out_N, np * sizeof(int32_t)))) return rc;
@@ -1641,12 +1691,24 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     HIPCHK(c, hipMemsetAsync(aji, 0, np * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(S, 0, np * sizeof(double), c->stream));
     HIPCHK(c, hipMemsetAsync(N, 0, np * sizeof(int32_t), c->stream));
+    const auto t1 = clk::now();
     rc = pfaai_run(c, 0, c->n_rows, flags | PFAAI_FLAG_EMIT_JAC, aji, S, N, c->stream);
     if (rc) return rc;
-    if (h_aji && (rc = d2h_staged(c, h_aji, aji, np * sizeof(double), c->stream))) return rc;
-    if (h_S && (rc = d2h_staged(c, h_S, S, np * sizeof(double), c->stream))) return rc;
-    if (h_N && (rc = d2h_staged(c, h_N, N, np * sizeof(int32_t), c->stream))) return rc;
+    const auto t2 = clk::now();
+    const bool trace = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    if (trace) HIPCHK(c, hipStreamSynchronize(c->stream));
+    const auto t3 = clk::now();
+    if (h_aji && (rc = staged_copy(c, h_aji, aji, np * sizeof(double), false, c->stream))) return rc;
+    const auto t4 = clk::now();
+    if (h_S && (rc = staged_copy(c, h_S, S, np * sizeof(double), false, c->stream))) return rc;
+    if (h_N && (rc = staged_copy(c, h_N, N, np * sizeof(int32_t), false, c->stream))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const auto t5 = clk::now();
+    if (trace) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[pfaai_compute] alloc+memset %.2f, run submit %.2f, run wait %.2f, D2H aji %.2f, S+N %.2f ms\n",
+                     ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5));
+    }
     return PFAAI_RC_OK;
 }
 
@@ -2196,9 +2258,9 @@ int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, dou
     }
     rc = pfaai_run(c, rb, re, flags | PFAAI_FLAG_EMIT_JAC, aji - f, S - f, N - f, c->stream);
     if (rc) return rc;
-    if (h_aji && (rc = d2h_staged(c, h_aji + f, aji, n * sizeof(double), c->stream))) return rc;
-    if (h_S && (rc = d2h_staged(c, h_S + f, S, n * sizeof(double), c->stream))) return rc;
-    if (h_N && (rc = d2h_staged(c, h_N + f, N, n * sizeof(int32_t), c->stream))) return rc;
+    if (h_aji && (rc = staged_copy(c, h_aji + f, aji, n * sizeof(double), false, c->stream))) return rc;
+    if (h_S && (rc = staged_copy(c, h_S + f, S, n * sizeof(double), false, c->stream))) return rc;
+    if (h_N && (rc = staged_copy(c, h_N + f, N, n * sizeof(int32_t), false, c->stream))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PFAAI_RC_OK;
 }

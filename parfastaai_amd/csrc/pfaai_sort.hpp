@@ -120,8 +120,10 @@ struct DstRecs {
 // set equality is proven by keyed hash sums: the sum over F of h(g * P + p,
 // t) (k_hash_f, streaming F block by block) must equal the sum over G of
 // h(list, G_tet) (k_gend) -- in two lanes keyed by independent per-load
-// random seeds, so different sets agree with probability ~2^-128 (h is a
-// 64-bit mix of the injective 50-bit code key << 18 | t).  So the sort's passes load nothing
+// random seeds and mixed by two different functions, so a different set has
+// to make both 64-bit sums agree at once (h is a 64-bit mix of the injective
+// 50-bit code key << 18 | t; one-multiply mixers are not a proven universal
+// family, so the ~2^-128 is heuristic).  So the sort's passes load nothing
 // beyond their records (the first form checked list bounds by G_off[key],
 // G_off[key + 1] and read G_tet[pos] per record in the last pass: ~3 random
 // L2 requests per record, 3.4 ms of a 10k load's pass).
@@ -129,13 +131,26 @@ struct DstRecs {
 // both Z_2^64 and GF(2)^64): one 64-bit multiply per lane -- the check runs
 // two lanes over every F and G entry beside the sort, and splitmix64's two
 // multiplies per lane made it the load's largest side cost (2.8 ms at 10k)
+// The two lanes use different mixers (shifts and multiplier), so lane 2 is
+// not lane 1 applied to a re-keyed code: a swap of one tetramer between two
+// lists -- codes {c, c^d1^d2} against {c^d1, c^d2}, an XOR parallelogram --
+// has to cancel in two unrelated functions (tests/test_gpu_load_sort.py swaps
+// tetramers between two genomes' lists and between two proteins' lists).
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 32;
     x *= 0xD6E8FEB86659FD93ull;
     return x ^ (x >> 32);
 }
+__device__ __forceinline__ uint64_t mix64b(uint64_t x) {
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
+    return x ^ (x >> 31);
+}
 __device__ __forceinline__ uint64_t member_hash(uint64_t seed, uint32_t key, uint32_t t) {
     return mix64(seed ^ (((uint64_t)key << 18) | t));  // key < 2^32, t < 2^18 (host-checked): injective
+}
+__device__ __forceinline__ uint64_t member_hash_b(uint64_t seed, uint32_t key, uint32_t t) {
+    return mix64b(seed ^ (((uint64_t)key << 18) | t));
 }
 
 struct DstGpos {
@@ -154,7 +169,7 @@ struct DstGpos {
 // every tetramer block t (one workgroup per block, grid-stride; four entries
 // per thread in flight, indices clamped rather than loads under a branch)
 // Two lanes (seed, seed2: independent per-load random keys; sums[0] and
-// sums[2]): a different multiset passes both with probability ~2^-128.
+// sums[2]): a different multiset has to pass both lanes' sums at once.
 // [g_lo, g_hi): only the entries of those genomes (a rank's rows, pfaai_load_rows).
 __global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, const int32_t* __restrict__ Fp,
                                                 const int32_t* __restrict__ Fg, uint32_t P, uint64_t seed,
@@ -177,7 +192,7 @@ __global__ __launch_bounds__(256) void k_hash_f(const int64_t* __restrict__ Lp, 
             for (int u = 0; u < 4; ++u)
                 if (i0 + u * 256 < e && in[u]) {
                     acc += member_hash(seed, key[u], (uint32_t)t);
-                    acc2 += member_hash(seed2, key[u], (uint32_t)t);
+                    acc2 += member_hash_b(seed2, key[u], (uint32_t)t);
                 }
         }
     }
@@ -394,7 +409,7 @@ __global__ __launch_bounds__(NT) void k_fends_hist(const int32_t* __restrict__ F
             if (r < rn && (uint32_t)(g[k] - g_lo) < gspan) {
                 const uint32_t key = (uint32_t)g[k] * P + (uint32_t)p[k];
                 acc += member_hash(seed, key, t);
-                acc2 += member_hash(seed2, key, t);
+                acc2 += member_hash_b(seed2, key, t);
             }
         }
 #pragma unroll
@@ -550,7 +565,7 @@ __global__ __launch_bounds__(256) void k_hash_g(const int64_t* __restrict__ G_of
                     while (pr[j + 1] <= f) ++j;
                     const uint32_t key = (uint32_t)(L0 + j);  // = g * P + p
                     a += member_hash(seed, key, (uint32_t)t[u]);
-                    b += member_hash(seed2, key, (uint32_t)t[u]);
+                    b += member_hash_b(seed2, key, (uint32_t)t[u]);
                 }
             }
         }
@@ -1220,7 +1235,7 @@ __global__ __launch_bounds__(256) void k_gend(const int64_t* __restrict__ G_off,
                     if constexpr (END) G_end[k[u]] = v[u];
                     if constexpr (HASH) {
                         hm += member_hash(seed, li[u], (uint32_t)t[u]);
-                        hm2 += member_hash(seed2, li[u], (uint32_t)t[u]);
+                        hm2 += member_hash_b(seed2, li[u], (uint32_t)t[u]);
                     }
                 }
             }

@@ -300,11 +300,17 @@ int ingest(const AppParams& app, LoadG load_g, LoadF load_f, DBMetaData& meta, L
     }
     std::printf("Load (SQLite)       : %10.2f ms  (%s, %zu entries)\n", ms_since(t0), what,
                 arr.F.empty() ? arr.G_tet.size() : arr.F.size());
+    const auto& gc = pfaai_host::g_load_clock();
+    if (!arr.G_tet.empty() && gc.read_ns > 0 && gc.threads > 0)  // thread time over the reading threads
+        std::printf("  G-path threads    : %d; per thread <p>_genomes read %.1f ms, orientation check "
+                    "(<p>_tetras read + sums) %.1f ms\n",
+                    gc.threads.load(), gc.read_ns / 1e6 / gc.threads, gc.check_ns / 1e6 / gc.threads);
     return 0;
 }
 
-// The HIP runtime's first initialisation (~80 ms on the box) runs on a helper
-// thread while the main thread reads SQLite; run_and_print joins it first.
+// The HIP runtime's first initialisation (~80 ms on the box) and the engine's
+// contexts are made on a helper thread while the main thread reads SQLite;
+// run_and_print joins it first.
 static std::thread g_warm;
 static void warm_gpu_join() {
     if (g_warm.joinable()) g_warm.join();
@@ -377,9 +383,11 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         const double ms_ctor = std::chrono::duration<double, std::milli>(t1 - t0).count();
         std::printf("  breakdown         : context %.1f + load checks %.1f, H2D %.1f, device F/G %.1f ms; run %.1f ms = "
                     "run tables %.2f + %s %.2f + D2H / JAC fill %.1f ms\n"
-                    "  host side of run  : engine compute + D2H done at %.1f, initJAC (beside it) at %.1f, JAC fill %.1f ms\n",
+                    "  host side of run  : engine compute + D2H done at %.1f, initJAC %s %.1f, JAC fill %.1f ms\n",
                     ms_ctor - lc - lu - ld, lc, lu, ld, ms_run, impl.msBuild(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?",
-                    impl.msRows(), ms_run - impl.msBuild() - impl.msRows(), impl.msCompute(), impl.msIds(), impl.msFill());
+                    impl.msRows(), ms_run - impl.msBuild() - impl.msRows(), impl.msCompute(),
+                    impl.preparedAhead() ? "+ output pages (during construction) took" : "(beside it) done at", impl.msIds(),
+                    impl.msFill());
         if (app.pathToOutputFile.empty()) return 0;
         t1 = std::chrono::steady_clock::now();
         std::printf("Writing output with %lld query genomes and %lld target genomes. \n",
@@ -503,11 +511,10 @@ int main(int argc, char** argv) {  // main.cpp:337-356
     app.print();
     WarmGuard warm_guard;
     if (app.dumpPrefix.empty() && app.dumpGenomes.empty()) {
-        const int dev = app.devices.empty() ? app.device : app.devices.front();
+        const std::vector<int> devs = app.devices.empty() ? std::vector<int>{app.device} : app.devices;
         try {
-            g_warm = std::thread([dev] {
-                pfaai_ctx* c = nullptr;
-                if (pfaai_create(&c, dev) == PFAAI_RC_OK) pfaai_destroy(c);
+            g_warm = std::thread([devs] {  // the engine adopts these contexts (pfaai::prewarm_context)
+                for (int d : devs) pfaai::prewarm_context(d);
             });
         } catch (const std::system_error&) {  // no thread: the engine initialises HIP itself
         }

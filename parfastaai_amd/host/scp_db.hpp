@@ -21,6 +21,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <random>
@@ -310,6 +311,22 @@ inline int read_genome_lists(Conn& tc, const std::string& schema, const std::str
 // probability ~2^-128 per protein), plus the membership counts.  A protein
 // whose two tables disagree sends the whole DB through the `<p>_tetras`
 // path, so the output is the reference's either way.
+// Thread time (ns, summed over the reading threads) of the last G-path
+// load: reading the `<p>_genomes` lists, and the membership check (the G
+// side's sums and the `<p>_tetras` blobs read and summed) -- the CLI prints
+// both beside the load's wall time (the check's host cost).
+struct GLoadClock {
+    std::atomic<int64_t> read_ns{0}, check_ns{0};
+    std::atomic<int> threads{0};
+};
+inline GLoadClock& g_load_clock() {
+    static GLoadClock c;
+    return c;
+}
+inline int64_t ns_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
+}
+
 struct MemberSum {
     uint64_t n = 0, a = 0, b = 0;
     bool operator==(const MemberSum& o) const { return n == o.n && a == o.a && b == o.b; }
@@ -447,9 +464,15 @@ inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays
     std::vector<ProteinLists> lists(P);
     std::vector<char> sets(P, 1);
     const MemberSeeds sd = MemberSeeds::fresh();
+    GLoadClock& clk = g_load_clock();
+    clk.read_ns = 0;
+    clk.check_ns = 0;
+    clk.threads = 0;
 #pragma omp parallel
     {
+        clk.threads.fetch_add(1);
         Conn tc(path);
+        int64_t t_read = 0, t_check = 0;
 #pragma omp for schedule(dynamic, 1)
         for (int p = 0; p < P; ++p) {
             auto& r = lists[p];
@@ -457,16 +480,22 @@ inline int load_single_g(const std::string& path, DBMetaData& meta, LoadedArrays
                 r.err = 1;
                 continue;
             }
+            auto t0 = std::chrono::steady_clock::now();
             int rc = read_genome_lists(tc, "", meta.proteinSet[p], 0, G, r);
+            t_read += ns_since(t0);
             if (rc != SQLITE_OK) r.err = rc;
             if (r.err) continue;
             // both orientations hold exactly the same memberships
+            t0 = std::chrono::steady_clock::now();
             const MemberSum mg = genome_members(r, 0, r.gid.size(), 0, 0, (uint32_t)p, sd);
             bool ok = true;
             const MemberSum mt = tetras_members(tc, "", meta.proteinSet[p], (uint32_t)p, G, sd, &rc, &ok);
+            t_check += ns_since(t0);
             if (rc != SQLITE_OK) r.err = rc;
             else sets[p] = ok && mg == mt && normalise_lists(r);
         }
+        clk.read_ns += t_read;
+        clk.check_ns += t_check;
     }
     for (int p = 0; p < P; ++p)
         if (lists[p].err) {

@@ -87,6 +87,38 @@ def test_both_given_refuses_a_g_that_is_not_the_transpose(engine):
     assert engine.load_info() == "g_checked"
 
 
+def _swap(G_off, G_tet, la, lb):
+    """G_tet with one tetramer of list la exchanged for one of list lb (each
+    absent from the other list): same G_off, every list still ascending --
+    the memberships {(la, t1), (lb, t2)} become {(la, t2), (lb, t1)}, an XOR
+    parallelogram of the check's codes."""
+    A = G_tet[G_off[la]:G_off[la + 1]].tolist()
+    B = G_tet[G_off[lb]:G_off[lb + 1]].tolist()
+    t1 = next(t for t in A if t not in set(B))
+    t2 = next(t for t in B if t not in set(A))
+    out = G_tet.copy()
+    out[G_off[la]:G_off[la + 1]] = sorted([t for t in A if t != t1] + [t2])
+    out[G_off[lb]:G_off[lb + 1]] = sorted([t for t in B if t != t2] + [t1])
+    return out
+
+
+@pytest.mark.parametrize("rows", [None, (40, 90)])
+def test_both_given_refuses_swapped_tetramers(engine, rows):
+    """One tetramer exchanged between two genomes' lists of one protein, and
+    between two proteins' lists of one genome: |G|, G_off and every list
+    length are unchanged, so only the membership sums can see it -- refused
+    by a full load and by a rank load whose block holds the lists."""
+    P = 24
+    pb = _problem(300, P, clade_size=10)
+    G_off, G_tet = pb["G_off"], pb["G_tet"]
+    load = (lambda **kw: engine.load(**kw)) if rows is None else (lambda **kw: engine.load(rows=rows, **kw))
+    for la, lb in ((50 * P + 3, 61 * P + 3), (70 * P + 2, 70 * P + 9)):
+        with pytest.raises(_capi.PfaaiError):
+            load(**dict(pb, G_tet=_swap(G_off, G_tet, la, lb)))
+    load(**pb)
+    assert engine.load_info() == "g_checked"
+
+
 def test_both_given_without_gpos_checks_membership_without_a_sort(engine):
     """Where the row kernels use no G_pos (-q subsets; all-vs-all past 20 480
     genomes) the both-given load runs only the membership sums (k_hash_f over

@@ -68,6 +68,9 @@ def main():
         if p.returncode:
             print(out[-3000:], err[-3000:], file=sys.stderr)
             raise SystemExit(f"{cmd[0]} exited {p.returncode}")
+        for l in err.splitlines():  # PFAAI_TRACE_COMPUTE=1: the library's phase lines
+            if l.startswith("[pfaai_"):
+                print(f"[e2e] {os.path.basename(cmd[0])} {l}", file=sys.stderr, flush=True)
         return w, [l.strip() for l in out.splitlines() if ":" in l and ("ms" in l or "time" in l.lower())]
 
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
