@@ -83,7 +83,18 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
     for (int i = 0; i < 2 * nt; ++i)
         if (!c->stage_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
     std::vector<hipError_t> err((size_t)nt, hipSuccess);
+    // PFAAI_TRACE_COMPUTE: per thread, ns in the copy API calls, the event
+    // waits and the host memcpy
+    static const bool trace = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    std::vector<int64_t> tr((size_t)nt * 4, 0);
+    using tclk = std::chrono::steady_clock;
+    const auto t_begin = tclk::now();
+    auto ns_of = [](tclk::time_point a) {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tclk::now() - a).count();
+    };
     auto slice = [&](int t) {
+        const auto t_slice = tclk::now();
+        int64_t* T = &tr[(size_t)t * 4];
         // [lo, hi) of the transfer, in slots of kStageSlot
         const size_t lo = bytes * (size_t)t / (size_t)nt, hi = bytes * (size_t)(t + 1) / (size_t)nt;
         char* pin[2] = {static_cast<char*>(c->stage_host) + (2 * (size_t)t) * kStageSlot,
@@ -105,19 +116,25 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
                 if ((size_t)j < ns) e = hipEventSynchronize(ev[j]);
         } else {
             auto out = [&](size_t k) -> hipError_t {
+                auto t0 = tclk::now();
                 hipError_t r = hipEventSynchronize(ev[k & 1]);
+                if (trace) T[1] += ns_of(t0), t0 = tclk::now();
                 if (r == hipSuccess) std::memcpy(static_cast<char*>(dst) + lo + k * kStageSlot, pin[k & 1], len(k));
+                if (trace) T[2] += ns_of(t0);
                 return r;
             };
             for (size_t k = 0; k < ns && e == hipSuccess; ++k) {
+                const auto t0 = tclk::now();
                 e = hipMemcpyAsync(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k),
                                    hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipEventRecord(ev[k & 1], s);
+                if (trace) T[0] += ns_of(t0);
                 if (e == hipSuccess && k >= 1) e = out(k - 1);  // slot k - 1 out while slot k's DMA runs
             }
             if (e == hipSuccess) e = out(ns - 1);
         }
         err[(size_t)t] = e;
+        if (trace) T[3] = ns_of(t_slice);
     };
     std::vector<std::thread> th;
     int started = 1;
@@ -128,6 +145,14 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
     slice(0);
     for (auto& x : th) x.join();
     for (int t = started; t < nt; ++t) slice(t);  // threads that could not be started
+    if (trace) {
+        int64_t mx[4] = {0, 0, 0, 0};
+        for (int t = 0; t < nt; ++t)
+            for (int j = 0; j < 4; ++j) mx[j] = std::max(mx[j], tr[(size_t)t * 4 + j]);
+        std::fprintf(stderr, "[pfaai_staged] %s %zu B, %d threads: wall %.2f ms; max per thread: api %.2f, wait %.2f, "
+                     "memcpy %.2f, slice %.2f ms\n", to_device ? "H2D" : "D2H", bytes, nt, ns_of(t_begin) / 1e6,
+                     mx[0] / 1e6, mx[1] / 1e6, mx[2] / 1e6, mx[3] / 1e6);
+    }
     for (hipError_t e : err) HIPCHK(c, e);
     return PFAAI_RC_OK;
 }

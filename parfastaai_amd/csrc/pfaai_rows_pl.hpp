@@ -202,7 +202,7 @@ constexpr int kClkBlocks = 256;
 // quirk) can give d < c, d <= 0: it takes per-column
 // branches with exact_div_any.  (An LDS table of RN(1/d) -- q = c * r plus
 // one residual correction is exact -- measured slower: 5.28 -> 6.13 ms on
-// the KW 4 rows of 10k, profiles/r05b/ab_div_kw4.txt; the table reads queue
+// the KW 4 rows of 10k, profiles/r05/ab_s5_rcp_table_kw4.txt; the table reads queue
 // behind the member atomics in LDS.)
 // V (variant bits): 1 S5 divides both columns of a nonzero counter word (no
 // per-column branches: the SALU of six exec-mask updates per word); 2 the

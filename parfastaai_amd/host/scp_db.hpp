@@ -307,8 +307,9 @@ inline int read_genome_lists(Conn& tc, const std::string& schema, const std::str
 // protein, the multisets of memberships (genome, tetramer) of the two tables
 // are equal.  Both sides are folded into order-independent keyed sums of a
 // 64-bit mix of the injective code g << 32 | (p * 160000 + t), in two lanes
-// with independent per-run random seeds (a difference goes unnoticed with
-// probability ~2^-128 per protein), plus the membership counts.  A protein
+// with independent per-run random seeds and different mixers (a difference
+// has to cancel in both lanes at once; ~2^-128 per protein is a heuristic
+// figure, not a proof), plus the membership counts.  A protein
 // whose two tables disagree sends the whole DB through the `<p>_tetras`
 // path, so the output is the reference's either way.
 // Thread time (ns, summed over the reading threads) of the last G-path
@@ -342,18 +343,26 @@ struct MemberSeeds {
     }
 };
 
-inline uint64_t member_mix(uint64_t x) {  // splitmix64 finaliser (a bijection)
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+// One multiply per lane and two different xorshift-multiply-xorshift
+// bijections for the two lanes (the device check's mixers, pfaai_sort.hpp):
+// splitmix64's two multiplies per lane made the check ~40 % of the G path's
+// per-thread time at C2 (34 of 90 ms; round 5)
+inline uint64_t member_mix_a(uint64_t x) {
+    x ^= x >> 32;
+    x *= 0xD6E8FEB86659FD93ull;
+    return x ^ (x >> 32);
+}
+inline uint64_t member_mix_b(uint64_t x) {
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
     return x ^ (x >> 31);
 }
 
 inline void member_add(MemberSum& m, const MemberSeeds& sd, uint32_t g, uint32_t p, uint32_t t) {
     const uint64_t key = (uint64_t)g << 32 | (uint64_t)(p * (uint32_t)kNTetramers + t);
     m.n += 1;
-    m.a += member_mix(sd.a ^ key);
-    m.b += member_mix(sd.b ^ key);
+    m.a += member_mix_a(sd.a ^ key);
+    m.b += member_mix_b(sd.b ^ key);
 }
 
 // The largest protein count whose codes p * 160000 + t fit 32 bits.
