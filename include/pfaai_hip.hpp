@@ -110,11 +110,11 @@ inline void advise_huge(const void* p, std::size_t bytes) {
 
 // [0, n) over up to 16 host threads (the adapter's array conversions)
 template <class Fn>
-void par_range(int64_t n, Fn fn) {
+void par_range(int64_t n, Fn fn, int max_threads = 16) {
     // >= 64k elements per thread (a 2M-pair JAC fill ran on one thread at the
     // old 4M grain: round-4's C2 "D2H / JAC fill" 25.5 ms)
     const int nt = (int)std::max<int64_t>(
-        1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
+        1, std::min<int64_t>({(int64_t)max_threads, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
     std::vector<std::thread> th;
     int started = 0;
     try {
@@ -477,10 +477,13 @@ class ParFAAIHipImpl {
         alloc_outputs(n, m_S, m_N);
         double* S = m_S.get();
         int32_t* N = m_N.get();
+        // on 4 threads: this runs beside the upload's 16 copy threads, and the
+        // job's CPU quota (16 on the pool's boxes) throttles every thread of
+        // the process once the sum runs over it
         detail::par_range((int64_t)n, [&](int64_t lo, int64_t hi) {
             for (int64_t i = lo; i < hi; i += 512) S[i] = 0.0;  // one store a 4 KB page
             for (int64_t i = lo; i < hi; i += 1024) N[i] = 0;
-        });
+        }, 4);
         m_msIds = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         m_prepared = true;
     }

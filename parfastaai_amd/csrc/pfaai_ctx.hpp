@@ -206,7 +206,11 @@ template <typename T>
 inline int upload(pfaai_ctx* c, DevBuf& b, const T* src, size_t n) {
     int rc = ensure(c, b, n * sizeof(T));
     if (rc) return rc;
-    if (n * sizeof(T) >= ((size_t)4 << 20)) return staged_copy(c, b.p, src, n * sizeof(T), true, c->stream);
+    // 4 MB .. 512 MB through the pinned slots (the CLI's C2 G_tet, 230 MB:
+    // 15.6 -> 8.0 ms); above that the runtime's own pageable path is faster
+    // (the bench's 1.15-GB arrays: ~25 ms each against 38 staged, round 5)
+    const size_t nb = n * sizeof(T);
+    if (nb >= ((size_t)4 << 20) && nb <= ((size_t)512 << 20)) return staged_copy(c, b.p, src, nb, true, c->stream);
     if (n) HIPCHK(c, hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
     return PFAAI_RC_OK;
 }

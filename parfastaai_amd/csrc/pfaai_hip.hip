@@ -54,6 +54,26 @@ int par_for(int64_t n, Fn fn, int64_t work = -1) {
 // exclusive scan of n u32 -> u64 out[0..n] (out[n] = total)
 int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* out, hipStream_t s);
 
+// Device -> pinned host slot by the shader (staged_copy's D2H): 16-B loads
+// from HBM, 16-B stores over the host link into the mapped pinned slot, the
+// tail by bytes.  (hipMemcpyAsync into the slots: the first large D2H of a
+// run stalled 8-19 ms inside the copy calls -- the C2 CLI's AJI, 16 MB --
+// while a 4-KB copy just before it took 0.02 ms; round 5.)
+__global__ __launch_bounds__(256) void k_stage_d2h(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   uint64_t bytes) {
+    const uint64_t n16 = bytes >> 4;
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool al = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+    if (al) {
+        for (uint64_t i = i0; i < n16; i += step)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+        for (uint64_t i = (n16 << 4) + i0; i < bytes; i += step) dst[i] = src[i];
+    } else {
+        for (uint64_t i = i0; i < bytes; i += step) dst[i] = src[i];
+    }
+}
+
 }  // namespace
 
 // Copies between the caller's pageable host memory and the device, both ways
@@ -95,6 +115,10 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
     auto slice = [&](int t) {
         const auto t_slice = tclk::now();
         int64_t* T = &tr[(size_t)t * 4];
+        // (all on s: spreading the threads over three streams measured
+        // slower, the C2 CLI's G_tet 8.0 -> 9.6-11.5 ms, the bench's 1.15-GB
+        // arrays 38 -> 42-49 ms: the DMA queue is not the limit)
+        hipStream_t st = s;
         // [lo, hi) of the transfer, in slots of kStageSlot
         const size_t lo = bytes * (size_t)t / (size_t)nt, hi = bytes * (size_t)(t + 1) / (size_t)nt;
         char* pin[2] = {static_cast<char*>(c->stage_host) + (2 * (size_t)t) * kStageSlot,
@@ -109,8 +133,8 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
                 if (e != hipSuccess) break;
                 std::memcpy(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k));
                 e = hipMemcpyAsync(static_cast<char*>(dst) + lo + k * kStageSlot, pin[k & 1], len(k),
-                                   hipMemcpyHostToDevice, s);
-                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], s);
+                                   hipMemcpyHostToDevice, st);
+                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], st);
             }
             for (int j = 0; j < 2 && e == hipSuccess; ++j)
                 if ((size_t)j < ns) e = hipEventSynchronize(ev[j]);
@@ -125,9 +149,11 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
             };
             for (size_t k = 0; k < ns && e == hipSuccess; ++k) {
                 const auto t0 = tclk::now();
-                e = hipMemcpyAsync(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k),
-                                   hipMemcpyDeviceToHost, s);
-                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], s);
+                hipLaunchKernelGGL(k_stage_d2h, dim3(128), dim3(256), 0, st,
+                                   reinterpret_cast<const uint8_t*>(static_cast<const char*>(src) + lo + k * kStageSlot),
+                                   reinterpret_cast<uint8_t*>(pin[k & 1]), (uint64_t)len(k));
+                e = hipGetLastError();
+                if (e == hipSuccess) e = hipEventRecord(ev[k & 1], st);
                 if (trace) T[0] += ns_of(t0);
                 if (e == hipSuccess && k >= 1) e = out(k - 1);  // slot k - 1 out while slot k's DMA runs
             }
@@ -1707,6 +1733,19 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     int rc;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
+    // (trace) the job's CPU-quota throttling over this call: cgroup v2 cpu.stat
+    auto throttled_us = []() -> long long {
+        FILE* f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+        if (!f) return -1;
+        char key[64];
+        long long v = 0, r = -1;
+        while (std::fscanf(f, "%63s %lld", key, &v) == 2)
+            if (std::strcmp(key, "throttled_usec") == 0) r = v;
+        std::fclose(f);
+        return r;
+    };
+    const bool trace0 = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    const long long thr0 = trace0 ? throttled_us() : 0;
     if ((rc = ensure(c, c->out_aji, np * sizeof(double)))) return rc;
     if ((rc = ensure(c, c->out_S, np * sizeof(double)))) return rc;
     if ((rc = ensure(c, c->out_N, np * sizeof(int32_t)))) return rc;
@@ -1722,6 +1761,13 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     const auto t2 = clk::now();
     const bool trace = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
     if (trace) HIPCHK(c, hipStreamSynchronize(c->stream));
+    double probe_ms = 0.0;
+    if (trace && c->stage_host) {  // one 4-KB copy alone: is the first D2H after the run slow whatever its size?
+        const auto tp = clk::now();
+        HIPCHK(c, hipMemcpyAsync(c->stage_host, aji, 4096, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        probe_ms = std::chrono::duration<double, std::milli>(clk::now() - tp).count();
+    }
     const auto t3 = clk::now();
     if (h_aji && (rc = staged_copy(c, h_aji, aji, np * sizeof(double), false, c->stream))) return rc;
     const auto t4 = clk::now();
@@ -1731,8 +1777,11 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     const auto t5 = clk::now();
     if (trace) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[pfaai_compute] alloc+memset %.2f, run submit %.2f, run wait %.2f, D2H aji %.2f, S+N %.2f ms\n",
-                     ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5));
+        const long long thr1 = throttled_us();
+        std::fprintf(stderr, "[pfaai_compute] alloc+memset %.2f, run submit %.2f, run wait %.2f (4-KB D2H probe %.2f), "
+                     "D2H aji %.2f, S+N %.2f ms; cgroup CPU throttling during the call %.2f ms\n", ms(t0, t1), ms(t1, t2),
+                     ms(t2, t3) - probe_ms, probe_ms, ms(t3, t4), ms(t4, t5),
+                     thr0 >= 0 && thr1 >= 0 ? (thr1 - thr0) / 1e3 : -1.0);
     }
     return PFAAI_RC_OK;
 }

@@ -33,10 +33,11 @@ inline void advise_huge(const void* p, std::size_t bytes) {
     if (e > a + ((std::uintptr_t)1 << 21)) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
 }
 
-// fn(lo, hi) over [0, n) on up to 8 threads (>= 64k items each)
+// fn(lo, hi) over [0, n) on up to 4 threads (>= 64k items each): initJAC runs
+// beside the upload's copy threads (the job's CPU quota is 16 on the pool's boxes)
 template <class Fn>
 void par_items(int64_t n, Fn fn) {
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({4, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
     std::vector<std::thread> th;
     for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
     fn(0, n / nt);
