@@ -65,6 +65,10 @@ struct pfaai_ctx {
     // device-resident problem
     DevBuf T16, T16c;      // u16 T by column genome (k_rows_pl)
     int64_t max_glen = 0;  // longest (genome, protein) G list
+    // T[p][g] is the length of every list (g, p) (checked at load): then
+    // every denominator T[p][A] + T[p][B] - c of a row with entries in p is
+    // >= 1, which the WK 3 row kernel relies on (it divides without a clamp)
+    bool t_exact = false;
     DevBuf Fp16;
     DevBuf Lp, Fp, Fg, T, is_q, q_index, t_rank, row_of, row_genome, tcol_row, tcol_col, G_off, G_tet, G_pos, blk;
     DevBuf G_end;  // end of the F run of every G entry (the fallback builds, packed into G_pe)
@@ -239,7 +243,7 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
 // (k_blk_end) instead of k_blk's 16-B entries.  One predicate for the run
 // table build (run_mode) and the kernel choice (launch_pl).
 inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
-    return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pe && !c->windows &&
+    return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pe && c->t_exact && !c->windows &&
            c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
            !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");

@@ -1049,6 +1049,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
     const int64_t ng = (int64_t)ni * P;
     int64_t n_g = 0;
     c->max_glen = 0;
+    c->t_exact = false;
     if (in_g) {
         if (p.G_off[0] != 0) return fail(c, PFAAI_RC_INVALID, "G_off must start at 0");
         std::atomic<int> bad_off{0};
@@ -1059,23 +1060,28 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
         if (bad_off) return fail(c, PFAAI_RC_INVALID, "G_off must be non-decreasing");
         n_g = p.G_off[ng];
         if (n_g > kMaxF) return fail(c, PFAAI_RC_INVALID, "|G| must be <= 2^32 - 64");
-        std::atomic<int> bad_t{0}, bad_ord{0};
+        std::atomic<int> bad_t{0}, bad_ord{0}, t_diff{0};
         std::vector<int64_t> mx(16, 0);
         par_for(
             ng,
             [&](int64_t lo, int64_t hi, int th) {
                 int64_t m = 0;
+                bool td = false;
                 for (int64_t k = lo; k < hi; ++k) {
                     const int64_t b = p.G_off[k], e = p.G_off[k + 1];
                     m = std::max(m, e - b);
+                    const int64_t g = k / P, q = k - g * P;  // list k = (genome g, protein q)
+                    td = td || g >= p.t_cols || (int64_t)p.T[q * p.t_cols + g] != e - b;
                     for (int64_t i = b; i < e; ++i) {
                         if (p.G_tet[i] < 0 || p.G_tet[i] >= PFAAI_NTETRAMERS) { bad_t = 1; return; }
                         if (i > b && p.G_tet[i] <= p.G_tet[i - 1]) { bad_ord = 1; return; }
                     }
                 }
                 mx[th] = m;
+                if (td) t_diff = 1;
             },
             n_g);
+        c->t_exact = !t_diff;
         if (bad_t) return fail(c, PFAAI_RC_INVALID, "G_tet holds a tetramer id outside [0, 160000)");
         if (bad_ord) return fail(c, PFAAI_RC_INVALID, "every G list must be strictly ascending");
         for (int64_t m : mx) c->max_glen = std::max(c->max_glen, m);
@@ -1371,6 +1377,7 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
             return rc;
         } else {
             c->max_glen = tmax;
+            c->t_exact = true;  // G_off from T, every list bound verified against the sorted keys
             fp16_done = true;
             c->load_path = PFAAI_LOAD_G_FROM_F;
         }

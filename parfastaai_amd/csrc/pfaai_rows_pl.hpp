@@ -453,7 +453,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         };
         if ((V & 1) != 0 && !(MODE == 2 && compat)) {
             // both columns of a nonzero word: a zero counter divides 0 by
-            // max(d, 1) and adds an exact +0.0 (S >= +0)
+            // max(d, 1) and adds an exact +0.0 (S >= +0).  WK 3 runs only
+            // on loads whose T is every list's length (pl_uses_ends,
+            // t_exact): then d = T[p][A] + T[p][B] - c >= T[p][A] >= 1 for a
+            // row with entries in p, and the clamp (2 VALU a word) goes
 #pragma unroll
             for (int k = 0; k < KW; ++k) {
                 if (WK == 3 && wbase + k * NT >= ncw) break;
@@ -464,8 +467,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     ev += (uint32_t)(c0 + c1);
                     n_add(k, v);
-                    const int32_t d0 = max(ta + (int32_t)(tw[k] & 0xFFFFu) - c0, 1);
-                    const int32_t d1 = max(ta + (int32_t)(tw[k] >> 16) - c1, 1);
+                    int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
+                    if constexpr (WK != 3) {
+                        d0 = max(d0, 1);
+                        d1 = max(d1, 1);
+                    }
                     if constexpr ((V & 8) != 0) {
                         exact_div_pair(c0, d0, c1, d1, S[2 * k], S[2 * k + 1]);
                     } else {
