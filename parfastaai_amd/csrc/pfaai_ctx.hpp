@@ -246,7 +246,7 @@ inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
     return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pe && c->t_exact && !c->windows &&
            c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
-           !DIAG_ENV("PFAAI_PL_WK0") && !DIAG_ENV("PFAAI_PL_CLK");
+           !DIAG_ENV("PFAAI_PL_WK0");
 }
 
 // Row kernels for output rows [rb, re) (pfaai_launch.hpp; instantiated per

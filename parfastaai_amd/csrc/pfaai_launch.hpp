@@ -203,6 +203,14 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             const int32_t nchunks = (int32_t)ceil_div((int64_t)c->cols_run + 1, chunk);
             auto* sc = static_cast<unsigned long long*>(c->scalars.p);
             auto* clk = static_cast<unsigned long long*>(c->dbg.p);
+            // the shipped wide form (WK 3 when the walk bounds are loaded, V = kPlV; 64 VGPRs, no spills
+            // with the clock registers), all rows as 1024-thread workgroups
+            if (pl_uses_ends(c, 0)) {
+                hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, 3, kPlV>), dim3(re - rb, 1), dim3(1024),
+                                   (pl_lds_bytes<5, 1024, 1>(c->prob.n_prot)), s, c->dev, rb, chunk, -1, flags,
+                                   sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
+                return;
+            }
             hipLaunchKernelGGL((k_rows_pl<0, 5, 1024, 8, true, 1, false, 1, 0>), dim3(re - rb, nchunks), dim3(1024),
                                (pl_lds_bytes<5, 1024, 1>(c->prob.n_prot)), s, c->dev, rb, chunk, -1, flags,
                                sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
