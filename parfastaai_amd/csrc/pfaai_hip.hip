@@ -59,7 +59,7 @@ int scan_u32(pfaai_ctx* c, const uint32_t* in, int64_t n, unsigned long long* ou
 // tail by bytes.  (hipMemcpyAsync into the slots: the first large D2H of a
 // run stalled 8-19 ms inside the copy calls -- the C2 CLI's AJI, 16 MB --
 // while a 4-KB copy just before it took 0.02 ms; round 5.)
-__global__ __launch_bounds__(256) void k_stage_d2h(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+__global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                    uint64_t bytes) {
     const uint64_t n16 = bytes >> 4;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
@@ -132,6 +132,9 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
                 if (k >= 2) e = hipEventSynchronize(ev[k & 1]);  // slot k & 1's previous DMA done
                 if (e != hipSuccess) break;
                 std::memcpy(pin[k & 1], static_cast<const char*>(src) + lo + k * kStageSlot, len(k));
+                // (the slot -> device step by the copy kernel instead: no
+                // change to the first step's clock and slower above 512 MB,
+                // profiles/r05/ab_h2d_kernel.txt)
                 e = hipMemcpyAsync(static_cast<char*>(dst) + lo + k * kStageSlot, pin[k & 1], len(k),
                                    hipMemcpyHostToDevice, st);
                 if (e == hipSuccess) e = hipEventRecord(ev[k & 1], st);
@@ -149,7 +152,7 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
             };
             for (size_t k = 0; k < ns && e == hipSuccess; ++k) {
                 const auto t0 = tclk::now();
-                hipLaunchKernelGGL(k_stage_d2h, dim3(128), dim3(256), 0, st,
+                hipLaunchKernelGGL(k_stage_copy, dim3(128), dim3(256), 0, st,
                                    reinterpret_cast<const uint8_t*>(static_cast<const char*>(src) + lo + k * kStageSlot),
                                    reinterpret_cast<uint8_t*>(pin[k & 1]), (uint64_t)len(k));
                 e = hipGetLastError();
