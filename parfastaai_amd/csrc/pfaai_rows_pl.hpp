@@ -527,7 +527,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         uint32_t* acc_i = acc + st * W;
         const bool has_i = i < P && glen(i) > 0u;
         // S5 first: it waits only for loads of the previous iteration (T
-        // words, and with KW = 5 the reloads of spilled registers, if any)
+        // words, and with KW = 5 the reloads of spilled registers, if any).
+        // (S5 after the first member round's issue, so those loads land
+        // while it computes, spills 12 VGPRs at KW = 5: the round's 8
+        // member registers live across S5's fp64 temporaries; round 5.)
         s5(i, twc, i >= 1 ? (int32_t)uni_u32(taL[i - 1]) : 0);
         stamp(7);
         const int pt = min(i, P - 1);
