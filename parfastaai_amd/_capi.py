@@ -19,10 +19,11 @@ except Exception:  # pragma: no cover - torch is optional for the binding
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PFAAI_HIP_LIB", os.path.join(_HERE, "lib", "libpfaai_hip.so"))
 # the same engine built with -DPFAAI_DIAGNOSTICS: the A/B switches (PFAAI_ROWS_KERNEL,
-# PFAAI_PL_WINDOWS, ...) and k_rows_v2 exist only here (tests of the variants, tools/gpu)
+# PFAAI_PL_WINDOWS, PFAAI_PL_V, ...) exist only here (tests of the variants, tools/gpu)
 DIAG_LIB_PATH = os.path.join(_HERE, "lib", "libpfaai_hip_diag.so")
 
 NTETRAMERS = 160000
+ABI_VERSION = 6  # PFAAI_ABI_VERSION of include/pfaai_hip.h
 PFAAI_OK = 0
 ERR_NAMES = {1: "SQLITE_DB", 2: "SQLITE_MEM_ALLOC", 3: "CONSTRUCT", 4: "HIP", 5: "OOM", 6: "RCCL", 7: "INVALID"}
 MODE_ALL, MODE_QSUB, MODE_QT = 0, 1, 2

@@ -28,7 +28,12 @@ def test_library_exports_every_symbol():
 
 
 def test_abi_version():
-    assert _capi.load_library().pfaai_version() == 6
+    # the header, the binding and the library agree (__graft_entry__.build() asserts the last two)
+    import re
+
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pfaai_hip.h")).read()
+    v = int(re.search(r"#define PFAAI_ABI_VERSION (\d+)", hdr).group(1))
+    assert v == _capi.ABI_VERSION == _capi.load_library().pfaai_version() == 6
 
 
 def test_problem_struct_layout():
