@@ -10,9 +10,10 @@ namespace pfaai_impl {
 
 // k_rows_pl's variant bits for the WK 3 walks (pfaai_rows_pl.hpp V): the
 // release form kPlV; PFAAI_PL_V=0 selects round 4's form (diagnostics, A/B).
-// The other forms (column windows, -q, -r, full rows) take kPlVG's S5 bits
-// where they do not spill (MODE 2 compiles both S5 forms: 114 VGPRs spilled,
-// so -r keeps V 0); PFAAI_PL_VG=0 overrides (A/B).
+// The other forms (column windows, -q, -r, full rows) take kPlVG's S5 bits;
+// MODE 2 (-r) only without PFAAI_FLAG_REF_COMPAT, as V kPlVG | 64 (compat
+// compiled out: with both S5 forms in one kernel it spilled 114 VGPRs, none
+// without); PFAAI_PL_VG=0 overrides (A/B).
 constexpr int kPlV = 27;
 constexpr int kPlVG = 9;
 
@@ -37,8 +38,11 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, WKV, VV>), dim3(r1 - r0, gy), dim3(NT), lds, s, \
                        dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
         c->last_walk = gp ? PFAAI_WALK_GPOS : PFAAI_WALK_SPLITTERS;
-        constexpr int VG = MODE == 2 ? 0 : kPlVG;
-        const bool vg = VG != 0 && !(DIAG_ENV("PFAAI_PL_VG") && atoi(DIAG_ENV("PFAAI_PL_VG")) == 0);
+        // MODE 2 (-r): kPlVG's bits only with the reference-compat quirk off,
+        // compiled out (V bit 64); with it, V 0
+        constexpr int VG = MODE == 2 ? (kPlVG | 64) : kPlVG;
+        const bool vg = VG != 0 && !(MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT)) &&
+                        !(DIAG_ENV("PFAAI_PL_VG") && atoi(DIAG_ENV("PFAAI_PL_VG")) == 0);
         if (wk == 0 || abs_chunk >= 0) {
             c->last_walk = PFAAI_WALK_SPLITTERS;
             if (vg) {

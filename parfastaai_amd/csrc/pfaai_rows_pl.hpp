@@ -208,7 +208,10 @@ constexpr int kClkBlocks = 256;
 // per-column branches: the SALU of six exec-mask updates per word); 2 the
 // WK 3 member scatter by pl_scatter8_code over k_fcode's member codes; 8
 // S5's two divisions of a word by one reciprocal (exact_div_pair, with 1);
-// 16 the G entries one protein ahead instead of two (WK 3, ONE below).  The
+// 16 the G entries one protein ahead instead of two (WK 3, ONE below); 64
+// the reference-compat quirks compiled out (MODE 2 launches it only without
+// PFAAI_FLAG_REF_COMPAT: its per-column general division then leaves the
+// kernel, and V 9 fits 64 VGPRs -- with it, 114 spilled).  The
 // WK 3 launches take V = 27 (pfaai_launch.hpp kPlV), the other forms V = 0.
 // Measured (tools/gpu/ab_rows.py, 10k all-vs-all, single launches of the
 // diagnostics build, profiles/r05/ab_v_*.txt): V 0 -> 3: 8.11-8.24 -> 8.07
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int32_t wlo = max(cc0, clo), whi = min(chi, cc0 + chunk_cols);
     if (wlo >= whi) return;  // uniform
     const int32_t ncw = (whi - cc0 + 1) >> 1;
-    const bool compat = flags & 1u;
+    const bool compat = (V & 64) != 0 ? false : (flags & 1u) != 0;  // V 64: launched only without REF_COMPAT
     const uint32_t min_len = abs_chunk >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
     const uint32_t prio = (flags >> 16) & 3u;
     const int P = d.n_prot;
