@@ -84,11 +84,12 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
 // 16 ms), round 5.  Here up to kStageThreads host threads each own a
 // contiguous slice of the transfer and two kStageSlot-byte slots of the
 // context's pinned buffer (allocated by pfaai_create, so the CLI's helper
-// thread pays it beside the SQLite read): down, slot k's DMA is queued before
-// slot k - 1 is copied out to dst; up, slot k is filled from src while slot
-// k - 1's DMA runs.  The page faults of an untouched dst are taken by all
-// threads at once.  Work ordered before on stream s is waited for; on return
-// every byte has landed.
+// thread pays it beside the SQLite read): down, slot k is filled by the copy
+// kernel k_stage_copy before slot k - 1 is copied out to dst; up, slot k is
+// filled from src while slot k - 1's DMA runs.  The page faults of an
+// untouched dst are taken by all threads at once.  Work ordered before on
+// stream s is waited for; on return every byte has landed.  The threads all
+// use stream s (spread over three streams the copies were slower, round 5).
 int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t bytes, bool to_device, hipStream_t s) {
     if (bytes == 0) return PFAAI_RC_OK;
     if (!c->stage_host && hipHostMalloc(&c->stage_host, kStageBytes, hipHostMallocDefault) != hipSuccess)
