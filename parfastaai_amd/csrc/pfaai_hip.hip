@@ -1575,11 +1575,12 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
     if (hipHostMalloc(&c->stage_host, kStageBytes, hipHostMallocDefault) != hipSuccess) c->stage_host = nullptr;
     for (hipEvent_t& e : c->stage_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
-    // one small copy each way through the pinned buffer: the first
-    // device-to-host copy of a process cost ~10 ms (the CLI's C2 AJI D2H:
-    // 11-20 ms for 16 MB, then 4 ms for the next 24 MB; round 5)
+    // one slot-sized DMA copy each way now, on the creating thread: the first
+    // host-to-device DMA of a process costs ~8 ms of setup (without this the
+    // C2 CLI's load H2D went 8.6 -> 16.4 ms: its small uploads take the
+    // runtime's path, round 5)
     void* warm = nullptr;
-    if (c->stage_host && hipMalloc(&warm, kStageSlot) == hipSuccess) {  // a slot's size: the DMA engines' path
+    if (c->stage_host && hipMalloc(&warm, kStageSlot) == hipSuccess) {
         if (hipMemcpyAsync(warm, c->stage_host, kStageSlot, hipMemcpyHostToDevice, c->stream) == hipSuccess)
             (void)hipMemcpyAsync(c->stage_host, warm, kStageSlot, hipMemcpyDeviceToHost, c->stream);
         (void)hipStreamSynchronize(c->stream);
