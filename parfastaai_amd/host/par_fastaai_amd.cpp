@@ -319,9 +319,15 @@ struct WarmGuard {
     ~WarmGuard() { warm_gpu_join(); }
 };
 
+// end of the last printed phase (the CLI's teardown line measures from here)
+static std::chrono::steady_clock::time_point g_t_phases_end;
+static bool g_have_phases_end = false;
+
 template <typename DS>
 int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
+    const auto tw = std::chrono::steady_clock::now();
     warm_gpu_join();
+    std::printf("HIP init (helper)   : %10.2f ms  waited for after the load\n", ms_since(tw));
     auto t0 = std::chrono::steady_clock::now();
     try {
         const std::vector<int> devs = app.devices.empty() ? std::vector<int>{app.device} : app.devices;
@@ -400,6 +406,8 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         if (!app.binPrefix.empty())
             write_bin(app.binPrefix, impl.getJAC(), impl.getAJI(), M, ds.qrySetSize(), ds.tgtSetSize());
         std::printf("Output              : %10.2f ms\n", ms_since(t1));
+        g_t_phases_end = std::chrono::steady_clock::now();
+        g_have_phases_end = true;
     } catch (const pfaai::HipError& e) {
         std::cerr << "MI355X engine error " << e.code << ": " << e.what() << std::endl;
         return e.code;
@@ -530,6 +538,8 @@ int main(int argc, char** argv) {  // main.cpp:337-356
     } else {
         rc = parallel_qry2tgt_fastaai(app);
     }
+    if (g_have_phases_end)  // engine contexts destroyed, host arrays freed
+        std::printf("Teardown            : %10.2f ms\n", ms_since(g_t_phases_end));
     std::printf("Total (CLI)         : %10.2f ms  (engine teardown included)\n", ms_since(t_main));
     // Every output file is closed and every engine context destroyed (both
     // inside the total above); what is left is the HIP runtime's exit-time
