@@ -1560,17 +1560,17 @@ int pfaai_create(pfaai_ctx** out, int device_id) {
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
     for (hipEvent_t& e : c->load_ev)
         if (hipEventCreate(&e) != hipSuccess) e = nullptr;
-    // every code object of the library loaded now rather than at the first
-    // launch of one of its kernels (HIP's deferred loading), so no caller's
-    // first run pays it (the CLI creates its first context on a thread during
-    // the SQLite read)
+    // the code objects of this file and of the all-vs-all row kernels loaded
+    // now rather than at the first launch of one of their kernels (HIP's
+    // deferred loading), so no all-vs-all caller's first run pays it (the CLI
+    // creates its context on a thread during the SQLite read).  The -q, -r
+    // and full-row translation units (pfaai_rows_m{1,2,3}, 20 MB) load at
+    // their first launch: preloading all four kept the C2 CLI waiting 129 ms
+    // for its helper thread after the load (round 5)
     {
         hipFuncAttributes a;
         (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_blk_end<1024, 1>));
         preload_rows<0>();
-        preload_rows<1>();
-        preload_rows<2>();
-        preload_rows<kModeFull>();
     }
     if (hipHostMalloc(&c->stage_host, kStageBytes, hipHostMallocDefault) != hipSuccess) c->stage_host = nullptr;
     for (hipEvent_t& e : c->stage_ev)
