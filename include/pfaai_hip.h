@@ -235,7 +235,11 @@ int pfaai_stream_events(const pfaai_ctx* ctx, int64_t* n_events);
  * Synchronous.  ALL and QT: disjoint row blocks have disjoint spans, so one
  * host thread per context (one context per device) fills a shared host
  * array for a multi-GPU run without a gather (CLI --devices; the C++
- * adapter's multi-device constructor).  QSUB: all rows only. */
+ * adapter's multi-device constructor).  QSUB (round 6): a block's cross
+ * cells are its contiguous span; its query-query cells (placed by query file
+ * index, owned by the pair's smaller genome id -- not contiguous) are
+ * merged into the triangle cell by cell, so the blocks of a split fill
+ * disjoint cells of one output. */
 int pfaai_compute_rows(pfaai_ctx* ctx, int64_t row_begin, int64_t row_end, uint32_t flags,
                        double* h_aji, double* h_S, int32_t* h_N);
 
@@ -310,9 +314,14 @@ int pfaai_run_info(const pfaai_ctx* ctx, int32_t* rows_kernel, int32_t* column_w
  *   GPOS       all-vs-all: from the row genome's own F position + 1 (G_pos)
  *              to its run end (G_end), both built at load -- the
  *              benchmarked form; no run table in the step
+ *   SPANS      column windows whose sub-runs hold only the row's partners
+ *              (all-vs-all windows past the row's first column, every
+ *              query-vs-target window): the window table's sub-run walked
+ *              whole, one launch over (row, window); the all-vs-all rows'
+ *              diagonal windows by the table + splitters
  * and whether the narrow rows (<= 2 047 columns) ran as a 512-thread launch
  * on the context's side stream beside the wide rows.  -1: no k_rows_pl ran. */
-enum { PFAAI_WALK_NONE = -1, PFAAI_WALK_SPLITTERS = 0, PFAAI_WALK_GPOS = 3 };
+enum { PFAAI_WALK_NONE = -1, PFAAI_WALK_SPLITTERS = 0, PFAAI_WALK_GPOS = 3, PFAAI_WALK_SPANS = 4 };
 int pfaai_run_walk(const pfaai_ctx* ctx, int32_t* walk, int32_t* narrow_launch);
 
 /* |E| of the last run, counted by the scatter kernel (equals the reference's

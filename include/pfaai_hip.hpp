@@ -140,6 +140,20 @@ inline bool prewarm_context(int device) {
     return true;
 }
 
+// Destroy the prewarmed contexts no engine adopted (e.g. the CLI's -q, which
+// runs on the first of its devices only): their pinned staging memory,
+// streams and buffers.  Returns how many were destroyed.
+inline int release_parked_contexts() {
+    detail::Parked& pk = detail::parked();
+    std::vector<std::pair<int, pfaai_ctx*>> left;
+    {
+        std::lock_guard<std::mutex> lk(pk.mu);
+        left.swap(pk.ctx);
+    }
+    for (auto& dc : left) pfaai_destroy(dc.second);
+    return (int)left.size();
+}
+
 // Contiguous row blocks over `parts` devices: cut[0] = 0 .. cut[parts] = n,
 // balanced by the row-cost model of parfastaai_amd/shard.py:split_rows (the
 // same cuts, pinned by tests/test_adapter_split.py): all-vs-all row a costs
@@ -214,19 +228,16 @@ struct pfaai_mode_of {
     }
 };
 
-// The producer half of the drop-in.  The reference's
-// DataStructInterface::construct() (interface.hpp:306-327) ends with
-// constructE(): the E array of every (protein, genome A, genome B) triple
-// (ds_helper.hpp:362-421) and its comparison sort (psort.hpp:27-53), 86 % of
-// the reference's wall time at C2.  The engine never reads E (refE()), so
-// DeviceE<DS> keeps every other construction step of DS -- the reference's
-// own ParFAAIData / ParFAAIQSubData / ParFAAIQryTgtData, constructors
-// inherited -- and makes constructE() return PFAAI_OK without building it.
-template <class DS>
-class DeviceE : public DS {
+// Side channel to the engine adapter (ParFAAIHipImpl::upload), which sees
+// its DSIT through the reference's abstract interface: a producer that holds
+// the genome-major `<p>_genomes` lists (pfaai::DeviceE, pfaai_dropin.hpp)
+// hands them over by a cross-cast, and the device builds F from them.
+class GenomeMajorSource {
   public:
-    using DS::DS;
-    auto constructE() -> decltype(std::declval<DS&>().constructE()) override { return {}; }
+    virtual ~GenomeMajorSource() = default;
+    // the (genome, protein) lists, list (g, p) at g * P + p; nullptr: none
+    virtual const std::vector<int64_t>* genomeMajorOff() const = 0;
+    virtual const std::vector<int32_t>* genomeMajorTet() const = 0;
 };
 
 template <typename IdType, typename ValueType, typename DSIT>
@@ -236,26 +247,30 @@ class ParFAAIHipImpl {
 
     // the drop-in: ParFAAIImpl(const DSIT&) (algorithm_impl.hpp:75-79), mode
     // deduced, reference-exact (ref_compat), device 0
+    // (ParFAAIImpl's callers continue with run() -- main.cpp:193-200, 256-264,
+    // 324-332 -- so this constructor prepares computeJAC's host outputs ahead)
     explicit ParFAAIHipImpl(const DSIT& ds)
-        : ParFAAIHipImpl(ds, pfaai_mode_of<DSIT>::deduce(ds), std::vector<int>{0}, true) {}
+        : ParFAAIHipImpl(ds, pfaai_mode_of<DSIT>::deduce(ds), std::vector<int>{0}, true, true) {}
     // mode: PFAAI_MODE_ALL / QSUB / QT (the three reference DSIT classes)
-    ParFAAIHipImpl(const DSIT& ds, int mode, int device = 0, bool ref_compat = false)
-        : ParFAAIHipImpl(ds, mode, std::vector<int>{device}, ref_compat) {}
+    ParFAAIHipImpl(const DSIT& ds, int mode, int device = 0, bool ref_compat = false, bool prepare_ahead = false)
+        : ParFAAIHipImpl(ds, mode, std::vector<int>{device}, ref_compat, prepare_ahead) {}
     // Multi-GPU (one process, one context per device, one host thread per
     // context): rows are split by the row-cost model of parfastaai_amd/shard.py
     // and every device writes its rows' JAC span of the shared host arrays
-    // (pfaai_compute_rows); ALL and QT -- QSUB runs on devices[0].
-    ParFAAIHipImpl(const DSIT& ds, int mode, const std::vector<int>& devices, bool ref_compat = false)
+    // (pfaai_compute_rows); ALL, QSUB and QT.
+    // prepare_ahead (opt-in, for callers that will call run() / computeJAC()
+    // and not stream): computeJAC's host side -- initJAC and the first touch
+    // of the output arrays, 44 B a pair -- on a helper thread while the
+    // contexts are made and the problem uploads, for outputs of up to
+    // kPrepPairs pairs: the CLI's C2 run phase was 21 ms of page faults and
+    // initJAC beside 1.6 ms of device work (round 5).  streamAJI /
+    // streamMatrix after it free what it prepared.
+    ParFAAIHipImpl(const DSIT& ds, int mode, const std::vector<int>& devices, bool ref_compat = false,
+                   bool prepare_ahead = false)
         : m_ds(ds), m_mode(mode), m_compat(ref_compat) {
         if (devices.empty()) throw HipError(PFAAI_RC_INVALID, "no device");
-        // computeJAC's host side -- initJAC and the first touch of the output
-        // arrays -- on a helper thread while the contexts are made and the
-        // problem uploads, when the outputs are small enough (<= kPrepPairs)
-        // that holding them from construction costs little: the CLI's C2
-        // run phase was 21 ms of page faults and initJAC beside 1.6 ms of
-        // device work (round 5)
         const int64_t np = (int64_t)ds.nGenomePairs();
-        if (np > 0 && np <= kPrepPairs) {
+        if (prepare_ahead && np > 0 && np <= kPrepPairs) {
             try {
                 m_prep.t = std::thread([this] {
                     try {
@@ -269,8 +284,7 @@ class ParFAAIHipImpl {
         }
         // contexts are owned by RAII handles: a throw below releases them
         m_ctx.push_back(detail::make_ctx(devices[0]));
-        for (std::size_t i = 1; i < devices.size() && mode != PFAAI_MODE_QSUB; ++i)
-            m_ctx.push_back(detail::make_ctx(devices[i]));
+        for (std::size_t i = 1; i < devices.size(); ++i) m_ctx.push_back(detail::make_ctx(devices[i]));
         upload();
     }
     ParFAAIHipImpl(const ParFAAIHipImpl&) = delete;
@@ -418,11 +432,19 @@ class ParFAAIHipImpl {
         pfaai_stream_events(ctx(), &m_events);
         return 0;
     }
-    const std::vector<JACType>& getJAC() const { return m_JAC; }
-    const std::vector<ValueType>& getAJI() const { return m_AJI; }
+    // (the accessors wait for the constructor's helper thread: it assigns m_JAC)
+    const std::vector<JACType>& getJAC() const {
+        wait_prep();
+        return m_JAC;
+    }
+    const std::vector<ValueType>& getAJI() const {
+        wait_prep();
+        return m_AJI;
+    }
     // the reference's debug listing (algorithm_impl.hpp:347-356; main.cpp
     // calls it when NDEBUG is not defined)
     void print_aji() const {
+        wait_prep();
         std::printf("AJI Ouput : \n [(GP1, GP2,   SUM, NCP) ->  AJI]\n");
         for (std::size_t i = 0; i < m_JAC.size(); ++i)
             std::printf(" [%lld, %.17g -> %03.2f] \n",
@@ -487,8 +509,12 @@ class ParFAAIHipImpl {
         m_msIds = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         m_prepared = true;
     }
-    void join_prep() {
+    // the helper thread finished (its error, if any, is rethrown by join_prep)
+    void wait_prep() const {
         if (m_prep.t.joinable()) m_prep.t.join();
+    }
+    void join_prep() {
+        wait_prep();
         if (m_prepErr) {
             std::exception_ptr e = m_prepErr;
             m_prepErr = nullptr;
@@ -534,18 +560,28 @@ class ParFAAIHipImpl {
     }
 
     void upload() {
-        const auto& Lc = m_ds.refLc();
-        const auto& F = m_ds.refF();
         const auto& T = m_ds.refT();
-        const int64_t nf = (int64_t)F.size();
         pfaai_problem pb{};
+        // a producer's genome-major lists (pfaai::DeviceE's `<p>_genomes`
+        // ingest): the device builds F from them, refF() is never asked
+        const GenomeMajorSource* gm = nullptr;
+        if constexpr (std::is_polymorphic<DSIT>::value) gm = dynamic_cast<const GenomeMajorSource*>(&m_ds);
+        if (gm && gm->genomeMajorOff() && gm->genomeMajorTet()) {
+            pb.G_off = gm->genomeMajorOff()->data();
+            pb.G_tet = gm->genomeMajorTet()->data();
+        }
+        const bool g_only = pb.G_off != nullptr;
+        static const std::vector<typename std::decay_t<decltype(m_ds.refF())>::value_type> kNoF;
+        const auto& F = g_only ? kNoF : m_ds.refF();
+        const int64_t nf = (int64_t)F.size();
         if constexpr (detail::has_genome_major<DSIT>::value) {
-            if (!m_ds.refGTet().empty() || nf == 0) {
+            if (!g_only && (!m_ds.refGTet().empty() || nf == 0)) {
                 pb.G_off = m_ds.refGOff().data();
                 pb.G_tet = m_ds.refGTet().data();
             }
         }
-        if (nf > 0 || !pb.G_off) {  // F in the reference's layout -> the ABI's columns
+        if (!g_only && (nf > 0 || !pb.G_off)) {  // F in the reference's layout -> the ABI's columns
+            const auto& Lc = m_ds.refLc();
             m_Lp.assign(PFAAI_NTETRAMERS + 1, 0);
             for (int t = 0; t < PFAAI_NTETRAMERS; ++t) m_Lp[t + 1] = m_Lp[t] + (int64_t)Lc[t];
             m_Fp.resize(nf);
@@ -630,7 +666,12 @@ class ParFAAIHipImpl {
         ~Joiner() {
             if (t.joinable()) t.join();
         }
-    } m_prep;
+    };
+    mutable Joiner m_prep;  // (joined by the const accessors too)
 };
 
 }  // namespace pfaai
+
+// the producer half of the drop-in: pfaai::DeviceE<DS> (it uses the adapter's
+// helpers above, and the adapter takes its lists through GenomeMajorSource)
+#include "pfaai_dropin.hpp"

@@ -46,7 +46,7 @@ EXPORTS = [
 GROUP_PEER_GATHER = 1  # pfaai_group_create_flags
 LOAD_PATHS = {0: "as_given", 1: "g_checked", 2: "g_from_f", 3: "f_from_g", 4: "legacy"}
 ROWS_KERNELS = {0: "pl", 1: "pl512", 2: "fused", 3: "worklist"}
-WALKS = {-1: "none", 0: "splitters", 3: "gpos"}  # pfaai_run_walk
+WALKS = {-1: "none", 0: "splitters", 3: "gpos", 4: "spans"}  # pfaai_run_walk
 
 # int sink(void* user, i64 row_begin, i64 row_end, i64 first, i64 count, const double* aji,
 #          const double* S, const int32_t* N)   (pfaai_sink_fn)

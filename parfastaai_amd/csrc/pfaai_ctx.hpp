@@ -249,6 +249,17 @@ inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
            !DIAG_ENV("PFAAI_PL_WK0");
 }
 
+// Column-window runs (c->windows) of all-vs-all and query-vs-target rows take
+// k_rows_pl WK 4 where a window's sub-run holds only the row's partners: one
+// launch over a grid of (row, window) with the member codes and no window
+// test -- all-vs-all windows past the row's first column, every
+// query-vs-target window (the tables stop at n_tgt); the all-vs-all rows'
+// diagonal windows take one WK 1 launch.  PFAAI_PL_NOWK4=1 (diagnostics)
+// keeps round 5's launch per window (A/B).
+inline bool pl_win_spans(pfaai_ctx* c, int mode) {
+    return c->windows && (mode == 0 || mode == 2) && c->rows_kernel == RK_PL && !DIAG_ENV("PFAAI_PL_NOWK4");
+}
+
 // Row kernels for output rows [rb, re) (pfaai_launch.hpp; instantiated per
 // mode in pfaai_rows_m{0,1,2}.hip).
 template <int MODE>

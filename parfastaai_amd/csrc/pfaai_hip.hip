@@ -104,9 +104,9 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
     for (int i = 0; i < 2 * nt; ++i)
         if (!c->stage_ev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
     std::vector<hipError_t> err((size_t)nt, hipSuccess);
-    // PFAAI_TRACE_COMPUTE: per thread, ns in the copy API calls, the event
-    // waits and the host memcpy
-    static const bool trace = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    // PFAAI_TRACE_COMPUTE (diagnostics build only): per thread, ns in the copy
+    // API calls, the event waits and the host memcpy
+    static const bool trace = DIAG_ENV("PFAAI_TRACE_COMPUTE") != nullptr;
     std::vector<int64_t> tr((size_t)nt * 4, 0);
     using tclk = std::chrono::steady_clock;
     const auto t_begin = tclk::now();
@@ -183,7 +183,14 @@ int pfaai_impl::staged_copy(pfaai_ctx* c, void* dst, const void* src, size_t byt
                      "memcpy %.2f, slice %.2f ms\n", to_device ? "H2D" : "D2H", bytes, nt, ns_of(t_begin) / 1e6,
                      mx[0] / 1e6, mx[1] / 1e6, mx[2] / 1e6, mx[3] / 1e6);
     }
-    for (hipError_t e : err) HIPCHK(c, e);
+    for (hipError_t e : err)
+        if (e != hipSuccess) {
+            // a failed slice may leave other slices' copy kernels or DMAs
+            // writing into the shared pinned slots: drain the stream before
+            // the caller reuses them
+            (void)hipStreamSynchronize(s);
+            return hip_fail(c, e, "staged_copy");
+        }
     return PFAAI_RC_OK;
 }
 
@@ -427,9 +434,19 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     if (c->windows) {
         if (!c->take_events()) return fail(c, PFAAI_RC_HIP, "hipEventCreate failed");
         HIPCHK(c, hipEventRecord(c->ev0, s));
-        // the window tables depend only on the loaded F and the window width
-        const bool keep = (flags & PFAAI_FLAG_KEEP_RUNS) && c->win_valid && c->win_cols == wcols &&
-                          (c->win_key || !compat);
+        // the window tables depend only on the loaded F and the window width:
+        // built by the first windowed run after a load, then kept by every
+        // later run of that load (a load product, like G_pe; round 6 -- the
+        // query-vs-target and streamed steps rebuilt them every run before)
+        const bool keep = c->win_valid && c->win_cols == wcols && (c->win_key || !compat);
+        // the WK 4 spans' member codes (pl_win_spans): k_fcode once per load
+        if (pl_win_spans(c, MODE) && !c->dev.Fcode) {
+            if (int rcf = ensure(c, c->Fcode, (size_t)(c->prob.n_f + 16) * sizeof(uint32_t))) return rcf;
+            hipLaunchKernelGGL(k_fcode, dim3((int)std::min<int64_t>(ceil_div(c->prob.n_f + 16, 256), 1 << 16)),
+                               dim3(256), 0, s, c->dev.Fg, c->prob.n_f, static_cast<uint32_t*>(c->Fcode.p));
+            HIPCHK(c, hipGetLastError());
+            c->dev.Fcode = static_cast<const uint32_t*>(c->Fcode.p);
+        }
         if (!keep) {
             Dev dw = c->dev;
             dw.blk = static_cast<uint4*>(c->blkw.p);
@@ -443,12 +460,14 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
             // (k_blk phase 2 off; PFAAI_BLK_QT_SPLIT=1 builds them, A/B)
             const char* qs = DIAG_ENV("PFAAI_BLK_QT_SPLIT");
             const int ph = MODE == 2 && !(qs && qs[0] == '1') ? 2 : 0;
+            // query vs target: the tables stop at n_tgt (targets only, WK 4)
+            const int32_t gmax = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
             if (bt && atoi(bt) == 256)
                 hipLaunchKernelGGL((k_blk<true, 256>), dim3(ceil_div(kNTetramers, win_tile)), dim3(256), lds, s, dw,
-                                   win_tile, ph, (int32_t)wcols, nwin);
+                                   win_tile, ph, (int32_t)wcols, nwin, gmax);
             else
                 hipLaunchKernelGGL((k_blk<true, 1024>), dim3(ceil_div(kNTetramers, win_tile)), dim3(1024), lds, s, dw,
-                                   win_tile, ph, (int32_t)wcols, nwin);
+                                   win_tile, ph, (int32_t)wcols, nwin, gmax);
             if (compat) {  // the zero-overlap quirk's first E triple (build_runs_g's second half)
                 const int rcf = launch_first_key(c, s);
                 if (rcf) return rcf;
@@ -1756,7 +1775,7 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
         std::fclose(f);
         return r;
     };
-    const bool trace0 = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    const bool trace0 = DIAG_ENV("PFAAI_TRACE_COMPUTE") != nullptr;
     const long long thr0 = trace0 ? throttled_us() : 0;
     if ((rc = ensure(c, c->out_aji, np * sizeof(double)))) return rc;
     if ((rc = ensure(c, c->out_S, np * sizeof(double)))) return rc;
@@ -1771,7 +1790,7 @@ int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int3
     rc = pfaai_run(c, 0, c->n_rows, flags | PFAAI_FLAG_EMIT_JAC, aji, S, N, c->stream);
     if (rc) return rc;
     const auto t2 = clk::now();
-    const bool trace = std::getenv("PFAAI_TRACE_COMPUTE") != nullptr;
+    const bool trace = DIAG_ENV("PFAAI_TRACE_COMPUTE") != nullptr;
     if (trace) HIPCHK(c, hipStreamSynchronize(c->stream));
     double probe_ms = 0.0;
     if (trace && c->stage_host) {  // one 4-KB copy alone: is the first D2H after the run slow whatever its size?
@@ -2319,14 +2338,62 @@ int pfaai_build_f(pfaai_ctx* c, const int32_t* prot, const int32_t* genome, cons
 // Rows into host arrays at their JAC span: one thread per context (device)
 // runs its own row block; the spans of disjoint row blocks are disjoint in
 // ALL and QT, so several devices fill one host JAC array without a gather.
+// A query-subset row block (ds_impl.hpp:251-305): rows [rb, re) are query
+// file indices.  Their nQ x nT cross cells are the contiguous span [rb * nT,
+// re * nT); their query-query cells lie in the triangle after all cross
+// rows, each pair owned by the row of its smaller genome id (isValidPair,
+// ds_impl.hpp:270-273) but placed by query file index -- not contiguous, and
+// not even confined to the block's rows when the -q list is not in id order
+// (SURVEY 8a row U).  So the block runs into a device copy of its hull with
+// the triangle's N preset to -1, the cross span is copied out directly, and
+// the triangle's written cells (N >= 0: every owned pair is written, zero
+// overlaps included) are merged into the caller's arrays -- the blocks of a
+// split own disjoint cells, so per-device threads may fill one output.
+static int compute_rows_qsub(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* h_aji, double* h_S,
+                             int32_t* h_N) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t nT = c->prob.n_tgt, f = rb * nT, tri0 = (int64_t)c->prob.n_qry * nT;
+    const int64_t n = c->n_pairs - f, ncross = (re - rb) * nT, ntri = c->n_pairs - tri0;
+    int rc;
+    if ((rc = ensure(c, c->out_aji, std::max<int64_t>(n, 1) * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_S, std::max<int64_t>(n, 1) * sizeof(double)))) return rc;
+    if ((rc = ensure(c, c->out_N, std::max<int64_t>(n, 1) * sizeof(int32_t)))) return rc;
+    auto* aji = static_cast<double*>(c->out_aji.p);
+    auto* S = static_cast<double*>(c->out_S.p);
+    auto* N = static_cast<int32_t*>(c->out_N.p);
+    HIPCHK(c, hipMemsetAsync(N + (tri0 - f), 0xFF, ntri * sizeof(int32_t), c->stream));
+    rc = pfaai_run(c, rb, re, flags | PFAAI_FLAG_EMIT_JAC, aji - f, S - f, N - f, c->stream);
+    if (rc) return rc;
+    if (h_aji && (rc = staged_copy(c, h_aji + f, aji, ncross * sizeof(double), false, c->stream))) return rc;
+    if (h_S && (rc = staged_copy(c, h_S + f, S, ncross * sizeof(double), false, c->stream))) return rc;
+    if (h_N && (rc = staged_copy(c, h_N + f, N, ncross * sizeof(int32_t), false, c->stream))) return rc;
+    if (ntri > 0) {
+        std::vector<double> ta((size_t)ntri), ts((size_t)ntri);
+        std::vector<int32_t> tn((size_t)ntri);
+        if ((rc = staged_copy(c, tn.data(), N + (tri0 - f), ntri * sizeof(int32_t), false, c->stream))) return rc;
+        if ((rc = staged_copy(c, ta.data(), aji + (tri0 - f), ntri * sizeof(double), false, c->stream))) return rc;
+        if ((rc = staged_copy(c, ts.data(), S + (tri0 - f), ntri * sizeof(double), false, c->stream))) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        par_for(ntri, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t i = lo; i < hi; ++i) {
+                if (tn[(size_t)i] < 0) continue;  // another block's cell
+                if (h_aji) h_aji[tri0 + i] = ta[(size_t)i];
+                if (h_S) h_S[tri0 + i] = ts[(size_t)i];
+                if (h_N) h_N[tri0 + i] = tn[(size_t)i];
+            }
+        });
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFAAI_RC_OK;
+}
+
 int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* h_aji, double* h_S,
                        int32_t* h_N) {
     if (!c) return PFAAI_RC_INVALID;
     if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
     if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
-    if (c->prob.mode == PFAAI_MODE_QSUB && !(rb == 0 && re == c->n_rows))
-        return fail(c, PFAAI_RC_INVALID, "pfaai_compute_rows: QSUB row blocks have no contiguous JAC span");
     if (rb == re) return PFAAI_RC_OK;
+    if (c->prob.mode == PFAAI_MODE_QSUB && !(rb == 0 && re == c->n_rows)) return compute_rows_qsub(c, rb, re, flags, h_aji, h_S, h_N);
     HIPCHK(c, hipSetDevice(c->device));
     int64_t f = 0, n = 0;
     pfaai_row_span(c, rb, re, &f, &n);

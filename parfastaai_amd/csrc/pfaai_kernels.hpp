@@ -358,6 +358,9 @@ constexpr int kBlkDynLds = kBlkLdsBytes - 256;
 // by genome), so a row-kernel launch over window w loads only the lines of
 // that window, and all its workgroups work on the same 1/nwin of F (L2 / MALL
 // locality).  The LDS staging then holds nwin tables (fewer tetramers per tile).
+// Ids >= gmax belong to no window (query vs target: gmax = n_tgt, so a window's
+// sub-run holds targets only -- every member a partner of a query row, the
+// row kernel's WK 4 span -- and no id can index past the nwin tables).
 __device__ __forceinline__ int32_t win_of(int32_t g, int32_t wcols, float inv) {
     int32_t w = (int32_t)((float)g * inv);  // g < 2^21: off by at most one, fixed below
     if (w * wcols > g) --w;
@@ -367,7 +370,7 @@ __device__ __forceinline__ int32_t win_of(int32_t g, int32_t wcols, float inv) {
 
 template <bool WIN = false, int NTH = kTetraThreads>
 __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32_t wcols = 0,
-                                                       int32_t nwin = 1) {
+                                                       int32_t nwin = 1, int32_t gmax = 0x7FFFFFFF) {
     // [nwin][kBlkTile][n_prot]: tetramer-major in LDS, so the heads / tails of
     // one tetramer's runs (consecutive proteins) land in different banks
     extern __shared__ uint4 ent[];
@@ -438,9 +441,10 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
             int wo = 0;  // window table offset
             if constexpr (WIN) {  // sub-runs by window: ids ascend along a run
                 const int32_t g = gg[j], gp = j == 0 ? gprev : gg[j - 1], gn = j == 7 ? gnext : gg[j + 1];
+                if (g >= gmax) continue;  // in no window (query-vs-target: the queries)
                 const int32_t w = win_of(g, wcols, inv);
                 head = head || gp < w * wcols;
-                tail = tail || gn >= (w + 1) * wcols;
+                tail = tail || gn >= min((w + 1) * wcols, gmax);
                 wo = w * PW;
             }
             if (head) ent[wo + tl * P + q].x = (uint32_t)i;
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(NTH) void k_blk(Dev d, int kBlkTile, int dbg, int32
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + (int64_t)u * NTH * kGroup;
-            if (i >= E) continue;
+            if (i >= E || (WIN && (int32_t)g[u] >= gmax)) continue;
             uint4* r = &ent[(WIN ? win_of((int32_t)g[u], wcols, inv) * PW : 0) + tet_of(i) * P + q[u]];
             const uint32_t k = (uint32_t)(i - (r->x & ~(uint32_t)(kGroup - 1))) / kGroup;  // line of the run
             if (k < 1 || k > (uint32_t)kSplitters) continue;

@@ -33,17 +33,17 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
     // all-vs-all rows in one chunk with G_pos loaded: each run walk starts just
     // past the row genome (k_rows_pl WK 3, pl_issue_m2<A8>)
     const bool gp = MODE == 0 && wk == 1 && pl_uses_ends(c, MODE);
-    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t abs_chunk) {
 #define PLK(BF, WKV, VV)                                                                                             \
     hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, false, NK, BF, WKV, VV>), dim3(r1 - r0, gy), dim3(NT), lds, s, \
-                       dv, r0, chunk, abs_chunk, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+                       dv, r0, chunk, ac, flags, sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS)
+    auto rows = [&](const Dev& dv, int64_t r0, int64_t r1, int32_t gy, int32_t ac) {
         c->last_walk = gp ? PFAAI_WALK_GPOS : PFAAI_WALK_SPLITTERS;
         // MODE 2 (-r): kPlVG's bits only with the reference-compat quirk off,
         // compiled out (V bit 64); with it, V 0
         constexpr int VG = MODE == 2 ? (kPlVG | 64) : kPlVG;
         const bool vg = VG != 0 && !(MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT)) &&
                         !(DIAG_ENV("PFAAI_PL_VG") && atoi(DIAG_ENV("PFAAI_PL_VG")) == 0);
-        if (wk == 0 || abs_chunk >= 0) {
+        if (wk == 0 || ac >= 0) {
             c->last_walk = PFAAI_WALK_SPLITTERS;
             if (vg) {
                 if (bigf) PLK(true, 0, VG); else PLK(false, 0, VG);
@@ -70,10 +70,42 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
                 if (bigf) PLK(true, kWk1, 0); else PLK(false, kWk1, 0);
             }
         }
-#undef PLK
     };
     if (nchunks == 1 || !c->windows) {
-        rows(c->dev, rb, re, nchunks, -1);
+        rows(c->dev, rb, re, nchunks, kWinRow);
+        return;
+    }
+    if (pl_win_spans(c, MODE)) {
+        // WK 4 (pl_win_spans): the windows whose sub-runs hold only partners
+        // as one launch over (row, window); all-vs-all rows' diagonal windows
+        // (the window of the row's first column, unless it starts there) as
+        // one WK 1 launch over the rows
+        const int64_t ncols = MODE == 2 ? c->prob.n_tgt : c->prob.n_ids;
+        const int32_t nwin = (int32_t)ceil_div(ncols, chunk);
+        // the first window some row of [rb, re) reaches from its start: a+1 <= w * chunk
+        const int32_t w_lo = MODE == 0 ? (int32_t)std::min<int64_t>(ceil_div(rb + 1, chunk), nwin) : 0;
+        c->last_walk = PFAAI_WALK_SPANS;
+        // the kernel offsets the window-major tables by its window index
+        Dev dv = c->dev;
+        dv.blk = static_cast<uint4*>(c->blkw.p);
+        constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2) : (kPlVG | 2);
+        const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 0: the QT quirk's per-column division
+        if (w_lo < nwin) {
+            const int64_t r0 = rb, r1 = re;
+            const int32_t ac = kWinGrid0 - w_lo;
+            const int32_t gy = nwin - w_lo;
+            if (bigf) {
+                if (cm) PLK(true, 4, 0); else PLK(true, 4, VS);
+            } else {
+                if (cm) PLK(false, 4, 0); else PLK(false, 4, VS);
+            }
+        }
+        if constexpr (MODE == 0) {
+            const int64_t r0 = rb, r1 = re;
+            const int32_t ac = kWinDiag;
+            const int32_t gy = 1;
+            if (bigf) PLK(true, 1, kPlVG); else PLK(false, 1, kPlVG);
+        }
         return;
     }
     // rows wider than one chunk (c->windows, set by run_mode, which built the
@@ -89,6 +121,7 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         dw.blk = static_cast<uint4*>(c->blkw.p) + (int64_t)w * c->prob.n_prot * kNTetramers;
         rows(dw, rb, r1, 1, w);
     }
+#undef PLK
 }
 
 // One k_rows_pl launch shape (KW, NT, WPE) with the N storage (nl: u8 in
@@ -130,7 +163,10 @@ void launch_k_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double*
 // an even column -- so two words per thread of 512 cover 2 047 columns)
 constexpr int kNarrowCols = 2 * 2 * 512 - 1;
 
-inline bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
+// (a template, instantiated by launch_rows<0> only: as a plain inline
+// function it instantiated the all-vs-all kernels in every mode's unit)
+template <int MODE>
+bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, double* S, int32_t* N,
                           hipStream_t s) {
     if (DIAG_ENV("PFAAI_PL_NO512") || !pl_uses_ends(c, 0) || !c->side_stream || !c->narrow_ev[0] || !c->narrow_ev[1])
         return false;
@@ -222,7 +258,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
         }
 #endif
         if constexpr (MODE == 0) {
-            if (nl && launch_narrow(c, rb, re, flags, aji, S, N, s)) return;
+            if (nl && launch_narrow<MODE>(c, rb, re, flags, aji, S, N, s)) return;
         }
         switch (kw) {
             case 1: launch_pl_n<MODE, 1, 1024, 8>(c, nl, rb, re, flags, aji, S, N, s); break;

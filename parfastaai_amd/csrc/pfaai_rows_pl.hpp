@@ -59,6 +59,10 @@ constexpr int kPlEntries = 1024;   // G entries per (genome, protein) (host-chec
 constexpr int kPlTaskCap = 4096;   // u16 line tasks per protein stage: run slot | line << 10
 constexpr int kPlMaxLines = 63;    // runs with more lines go to the whole-workgroup walk
 constexpr uint16_t kPlNoTask = 0xFFFFu;
+// k_rows_pl's column selection (its abs_chunk argument) besides a fixed
+// window index >= 0: per-row chunks, the row's diagonal window, or a grid
+// of windows over blockIdx.y starting at window kWinGrid0 - abs_chunk
+constexpr int32_t kWinRow = -1, kWinDiag = -2, kWinGrid0 = -3;
 
 // E triple (p, A, b): +1 into the u16 counter of column b (the
 // whole-workgroup walk of runs too long for line tasks).
@@ -77,7 +81,9 @@ __device__ __forceinline__ void pl_add(const Dev& d, int32_t a, int32_t b, uint3
 // test a member needs -- 0: wlo <= b < whi; 1: wlo <= b (the window reaches
 // the last id, e.g. an all-vs-all row in one chunk); 2: none (the window is
 // every id, e.g. a full row); 3: none (the members after A in a run,
-// all-vs-all with G_pos, see pl_issue_m2).
+// all-vs-all with G_pos, see pl_issue_m2); 4: none (a column window's
+// sub-run that holds only partners: all-vs-all windows past the row's
+// first column, query-vs-target windows, whose tables stop at n_tgt).
 template <int MODE, int WK>
 __device__ __forceinline__ void pl_add_m(const Dev& d, int32_t a, int32_t b, bool valid, uint32_t* accb, int32_t wlo,
                                          uint32_t wspan) {
@@ -249,15 +255,28 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int32_t a = d.row_genome[row_begin + rl];
     int32_t clo, chi;
     row_cols<MODE>(d, a, clo, chi);
-    // chunks start at even columns so a counter word / T word holds columns (2w, 2w+1);
-    // abs_chunk >= 0: one absolute column window [abs_chunk * chunk_cols, +chunk_cols),
-    // the one the run table was built for (k_blk<true>)
-    const int32_t cc0 = abs_chunk >= 0 ? abs_chunk * chunk_cols : (clo & ~1) + (int32_t)blockIdx.y * chunk_cols;
+    // chunks start at even columns so a counter word / T word holds columns (2w, 2w+1).
+    // abs_chunk (pl_win): >= 0 one absolute column window [abs_chunk * chunk_cols,
+    // +chunk_cols), the one the run table was built for (k_blk<true>); kWinRow per-row
+    // chunks blockIdx.y; kWinDiag the window holding the row's first column (all-vs-all:
+    // the rows' diagonal blocks, none where the row starts a window); <= kWinGrid0 the
+    // window (kWinGrid0 - abs_chunk) + blockIdx.y (all-vs-all: off-diagonal only, a row
+    // whose columns start past the window's start skips it).  With a window index the
+    // window's table is d.blk + w * P * 160000.
+    int32_t win = abs_chunk;
+    if (abs_chunk == kWinDiag) {
+        win = clo / chunk_cols;
+        if (MODE == 0 && clo == win * chunk_cols) return;  // uniform: the row starts a window (off-diagonal)
+    } else if (abs_chunk <= kWinGrid0) {
+        win = (kWinGrid0 - abs_chunk) + (int32_t)blockIdx.y;
+        if (MODE == 0 && clo > win * chunk_cols) return;  // uniform: the diagonal launch's (or no) columns
+    }
+    const int32_t cc0 = win >= 0 ? win * chunk_cols : (clo & ~1) + (int32_t)blockIdx.y * chunk_cols;
     const int32_t wlo = max(cc0, clo), whi = min(chi, cc0 + chunk_cols);
     if (wlo >= whi) return;  // uniform
     const int32_t ncw = (whi - cc0 + 1) >> 1;
     const bool compat = (V & 64) != 0 ? false : (flags & 1u) != 0;  // V 64: launched only without REF_COMPAT
-    const uint32_t min_len = abs_chunk >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
+    const uint32_t min_len = win >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
     const uint32_t prio = (flags >> 16) & 3u;
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
@@ -289,12 +308,16 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // Fg carries 16 padding entries and the range covers them: a 16-B load
     // that crosses num_records reads all zeros, not just its tail
     const rsrc_t r_fg = mk_rsrc(d.Fg, (uint64_t)(d.n_f + 16) * 4u);
-    constexpr bool CODE = (V & 2) != 0 && WK == 3 && MODE == 0;  // member loads read the codes (k_fcode)
+    // member loads read the codes (k_fcode): the WK 3 walks, and the WK 4 window
+    // spans (every member a partner: all-vs-all off-diagonal, query vs target)
+    constexpr bool CODE = (V & 2) != 0 && ((WK == 3 && MODE == 0) || (WK == 4 && (MODE == 0 || MODE == 2)));
     const rsrc_t r_fm = CODE ? mk_rsrc(d.Fcode, (uint64_t)(d.n_f + 16) * 4u) : r_fg;
     const int32_t* Fm = CODE ? reinterpret_cast<const int32_t*>(d.Fcode) : d.Fg;
     const rsrc_t r_g = mk_rsrc(d.G_tet + g0, (uint64_t)uni_u32(goff[P]) * 4u);
-    // the run table: 16-B entries (k_blk); unused by WK 3
-    const rsrc_t r_blk = mk_rsrc(d.blk, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked)
+    // the run table: 16-B entries (k_blk; a window's own table under a window
+    // grid); unused by WK 3
+    const uint4* blk_w = d.blk + (abs_chunk < kWinRow ? (int64_t)win * P * kNTetramers : 0);
+    const rsrc_t r_blk = mk_rsrc(blk_w, (uint64_t)P * kNTetramers * 16u);  // < 4 GiB: P <= 1600 (host-checked)
     const rsrc_t r_t16 = mk_rsrc(T16, (uint64_t)P * d.t16_cols * 2u);
     // S1 / S2 return the raw loads: nothing may touch a prefetched value
     // before its consumer, or the compiler waits for it on the spot.
@@ -366,8 +389,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             if constexpr (GP) {
                 r = make_uint2(gq2[j] + 1u, ONE ? (uint32_t)gt1[j] : r4[j].y);  // OOB entries: (1, 0), empty
                 nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
+            } else if constexpr (WK == 4) {
+                // the window sub-run is exactly A's partners in the window:
+                // 16-member tasks from an 8-aligned start, as WK 3
+                r = make_uint2(r4[j].x, r4[j].y);  // OOB entries: (0, 0), empty
+                nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
             } else {
-                nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && abs_chunk >= 0));
+                nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && win >= 0));
             }
             rt[st][e] = r;
             if (nl[j] > (uint32_t)kPlMaxLines) {
@@ -511,7 +539,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int grpx = tid >> 1;
     int st_cur = 0;
     auto issue2 = [&](int k, int ntk, uint4& bb, uint4& bbh) -> uint32_t {
-        return pl_issue_m2<TC, BIGF, GP>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
+        return pl_issue_m2<TC, BIGF, GP || WK == 4>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
     };
     auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
         if constexpr (CODE) {

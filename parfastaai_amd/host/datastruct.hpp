@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -35,12 +36,23 @@ inline void advise_huge(const void* p, std::size_t bytes) {
 
 // fn(lo, hi) over [0, n) on up to 4 threads (>= 64k items each): initJAC runs
 // beside the upload's copy threads (the job's CPU quota is 16 on the pool's boxes)
+// A slice whose thread cannot be created (std::system_error) runs on the
+// calling thread; the threads that did start are always joined.
 template <class Fn>
 void par_items(int64_t n, Fn fn) {
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({4, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
     std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
+    th.reserve(nt);
+    int started = 1;
+    try {
+        for (; started < nt; ++started) {
+            const int t = started;
+            th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
+        }
+    } catch (const std::system_error&) {
+    }
     fn(0, n / nt);
+    for (int t = started; t < nt; ++t) fn(n * t / nt, n * (t + 1) / nt);
     for (auto& x : th) x.join();
 }
 

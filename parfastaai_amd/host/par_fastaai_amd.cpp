@@ -331,7 +331,16 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
     auto t0 = std::chrono::steady_clock::now();
     try {
         const std::vector<int> devs = app.devices.empty() ? std::vector<int>{app.device} : app.devices;
-        pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, devs, app.refCompat);
+        // the run()-and-print path prepares its host outputs during construction
+        // (initJAC, output pages); the streamed paths never hold them
+        // the reference's QT rows overlap when nQ > nT (its column placement,
+        // ds_impl.hpp:434-436 + main.cpp:149, writes later rows over earlier
+        // ones): pfaai_stream_matrix cannot reproduce that tile by tile, so
+        // such a run takes the dense writer below (same bytes)
+        const bool stream_ok = !(mode == PFAAI_MODE_QT && app.refCompat && ds.qrySetSize() > ds.tgtSetSize());
+        const bool streamed = !app.streamAji.empty() || (app.streamCsv && stream_ok && !app.pathToOutputFile.empty());
+        pfaai::ParFAAIHipImpl<int32_t, double, DS> impl(ds, mode, devs, app.refCompat, !streamed);
+        pfaai::release_parked_contexts();  // prewarmed contexts no engine adopted
         if (!app.streamAji.empty()) {  // output-tile streaming: no CSV, no whole matrix anywhere
             if (mode == PFAAI_MODE_QSUB) {
                 std::cerr << "--stream-aji does not support -q" << std::endl;
@@ -342,11 +351,6 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
                         (long long)impl.nEvents(), app.streamAji.c_str());
             return rc;
         }
-        // the reference's QT rows overlap when nQ > nT (its column placement,
-        // ds_impl.hpp:434-436 + main.cpp:149, writes later rows over earlier
-        // ones): pfaai_stream_matrix cannot reproduce that tile by tile, so
-        // such a run takes the dense writer below (same bytes)
-        const bool stream_ok = !(mode == PFAAI_MODE_QT && app.refCompat && ds.qrySetSize() > ds.tgtSetSize());
         if (app.streamCsv && !stream_ok)
             std::printf("--stream-csv: -r with more query than target genomes reproduces the reference's overlapping "
                         "rows only through the dense writer; writing the CSV that way\n");
@@ -382,7 +386,7 @@ int run_and_print(const DS& ds, int mode, const AppParams& app, bool isSubset) {
         const int wf = impl.walkForm();
         std::printf("AJI (MI355X x%d)     : %10.2f ms  (|E| = %lld; %s; walk %s%s)\n", impl.nDevices(), ms_since(t0),
                     (long long)impl.nEvents(), rk >= 0 && rk < 5 ? kRowsKernelName[rk] : "?",
-                    wf == PFAAI_WALK_GPOS ? "G_pos..G_end" : wf == PFAAI_WALK_SPLITTERS ? "run table + splitters" : "-",
+                    wf == PFAAI_WALK_GPOS ? "G_pos..G_end" : wf == PFAAI_WALK_SPANS ? "window spans" : wf == PFAAI_WALK_SPLITTERS ? "run table + splitters" : "-",
                     impl.narrowLaunch() ? ", 512-thread narrow rows" : "");
         double lc = 0, lu = 0, ld = 0;
         pfaai_load_timing(impl.context(), &lc, &lu, &ld);

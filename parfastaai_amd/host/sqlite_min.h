@@ -5,6 +5,10 @@
 #pragma once
 #include <cstdint>
 
+// (a translation unit that already has the real sqlite3.h -- the reference's
+// main.cpp, which includes the drop-in adapter after it -- takes its
+// declarations and macros instead)
+#ifndef SQLITE3_H
 extern "C" {
 struct sqlite3;
 struct sqlite3_stmt;
@@ -36,4 +40,5 @@ constexpr int SQLITE_OPEN_READONLY = 0x00000001;
 constexpr int SQLITE_OPEN_URI = 0x00000040;
 constexpr int SQLITE_OPEN_READWRITE = 0x00000002;
 constexpr int SQLITE_OPEN_CREATE = 0x00000004;
+#endif
 #define PFAAI_SQLITE_TRANSIENT (reinterpret_cast<void (*)(void*)>(-1))

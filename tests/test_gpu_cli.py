@@ -76,7 +76,8 @@ def test_cli_qt_correct_equals_merged_db_block(tmp_path):
 def test_cli_vs_reference_binary_on_syn(tmp_path, case, devs):
     """The CLI's CSV equals the reference binary's, on one context and with the
     rows split over three contexts (--devices 0,0,0: the multi-GPU path, one
-    host thread per context, on the box's one GPU; -q runs on the first)."""
+    host thread per context, on the box's one GPU; -q too since round 6 --
+    each context's query-query cells merged into the triangle)."""
     import make_ref_vectors as mk
     kind, kw = mk.CASES[case]
     kw = dict(kw)
@@ -171,6 +172,10 @@ def test_cli_c1_rebuilt_db(tmp_path, compat):
     q = tmp_path / "q.txt"
     q.write_text(text("qsub_test_input.txt"))
     run(db, str(out), "-q", str(q), *compat)
+    assert out.read_text() == text("qsub_test_output_matrix_wheader.csv")
+    # -q with its query rows split over three contexts (round 6)
+    r = run(db, str(out), "-q", str(q), "--devices", "0,0,0", *compat)
+    assert "AJI (MI355X x3)" in r.stdout, r.stdout
     assert out.read_text() == text("qsub_test_output_matrix_wheader.csv")
 
 

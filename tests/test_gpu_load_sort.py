@@ -173,6 +173,28 @@ def test_f_only_inconsistent_t_takes_the_general_sort(engine):
     _check_rows(engine, pb, (0, 7, 100, 198), res)
 
 
+@pytest.mark.parametrize("given", ["both", "g_only"])
+def test_g_given_inconsistent_t_takes_the_clamped_walk(engine, given):
+    """the WK 3 walk divides without the denominator clamp, which
+    is safe only when T is every (genome, protein) list's length (t_exact,
+    checked at load).  G handed over (with F, or alone) with one T entry
+    larger than its list length: the load must not take the clamp-free
+    form -- the run takes the run table + splitters walk -- and S / N follow
+    the reference with that T (oracle, bit-exact)."""
+    pb = _problem(200, 16, clade_size=8)
+    T = pb["T"].copy()
+    T[3, 7] += 2
+    T[0, 150] += 1
+    pb = dict(pb, T=T)
+    if given == "g_only":
+        pb = _strip(pb, ("Lp", "F_prot", "F_genome"))
+    engine.load(**pb)
+    res = engine.compute(0)
+    assert engine.stats()["walk"] == "splitters", engine.stats()
+    full = pb if given == "both" else dict(_problem(200, 16, clade_size=8), T=T)
+    _check_rows(engine, full, (0, 3, 7, 100, 150, 198), res)
+
+
 def test_g_only_long_list(engine):
     """A (genome, protein) list of 9 000 tetramers: the G-only sort's records
     (tetramer | protein | genome) carry no list offset, so it still takes the

@@ -194,6 +194,53 @@ def test_column_windows_equal_row_chunks(diag_engine, monkeypatch, mode):
             assert np.array_equal(a3, a1) and np.array_equal(S3, S1) and np.array_equal(N3, N1)
 
 
+@pytest.mark.parametrize("case", ["all", "qt", "qt_edge"])
+def test_window_spans_equal_window_launches(diag_engine, monkeypatch, case):
+    """Round 6: column windows whose sub-runs hold only the row's partners
+    (all-vs-all windows past the row's first column, every query-vs-target
+    window) run as one WK 4 launch over (row, window) with the member codes
+    and no window test, the all-vs-all diagonal windows as one WK 1 launch
+    (pfaai_run_walk "spans") == round 5's launch per window over the window
+    tables (PFAAI_PL_NOWK4=1, diagnostics build) == the oracle on sampled
+    rows, S / N / AJI / |E| bit-exact, ref-compat included.  qt_edge: 20 480
+    targets = exactly two windows, so the query ids (>= n_tgt) lie past the
+    last window -- the tables stop at n_tgt, and no id indexes past them."""
+    engine = diag_engine
+    if case == "all":
+        pb = _all_problem(21000, 3, clade_size=50, n_random=1)
+        rows = [0, 10238, 10239, 10240, 15000, 20998]  # 10239: its columns start window 1
+    else:
+        n_tgt = 12000 if case == "qt" else 20480
+        pb = qt_syn(dict(n_tgt=n_tgt, n_qry=40, n_prot=4, clade_size=30, n_random=1), genome_major=True).problem()
+        rows = [n_tgt, n_tgt + 17, n_tgt + 39]
+    engine.load(**pb)
+    pr = O.Problem(pb)
+    res = {}
+    for flags in (0, _capi.FLAG_REF_COMPAT):
+        monkeypatch.delenv("PFAAI_PL_NOWK4", raising=False)
+        a1, S1, N1 = res[flags] = engine.compute(flags)
+        st = engine.stats()
+        assert st["walk"] == "spans", st
+        monkeypatch.setenv("PFAAI_PL_NOWK4", "1")
+        a2, S2, N2 = engine.compute(flags)
+        assert engine.stats()["walk"] == "splitters"
+        assert engine.stats()["n_events"] == st["n_events"]
+        assert np.array_equal(N1, N2) and np.array_equal(S1, S2) and np.array_equal(a1, a2)
+        monkeypatch.delenv("PFAAI_PL_NOWK4", raising=False)
+    n = pb["n_ids"]
+    _, S2, N2 = res[0]
+    for a in rows:
+        So, No, _ = pr.dense_rows(a, a + 1)
+        if case == "all":
+            b = np.arange(a + 1, n)
+            k = n * a + b - (a + 2) * (a + 1) // 2
+        else:
+            n_tgt = pb["n_tgt"]
+            b = np.arange(n_tgt)
+            k = (a - n_tgt) * n_tgt + b
+        assert np.array_equal(N2[k], No[0, b]) and np.array_equal(S2[k], So[0, b]), a
+
+
 def test_compute_rows_two_contexts_fill_one_array(engine):
     """pfaai_compute_rows: two contexts (here both on device 0) each write
     their row block's JAC span of one host array; == pfaai_compute."""
@@ -216,6 +263,43 @@ def test_compute_rows_two_contexts_fill_one_array(engine):
         assert np.array_equal(a, ref_a) and np.array_equal(S, ref_S) and np.array_equal(N, ref_N)
     finally:
         e2.close()
+
+
+@pytest.mark.parametrize("order", ["sorted", "shuffled"])
+def test_compute_rows_qsub_blocks_fill_one_array(engine, order):
+    """Round 6: -q row blocks through pfaai_compute_rows --
+    each block's cross cells by span, its query-query cells merged into the
+    triangle cell by cell -- fill one array equal to pfaai_compute, for a
+    query list in DB order and one shuffled (a pair's cell
+    then lies in another block's rows), ref-compat included; three contexts
+    on device 0 as in the CLI's --devices 0,0,0."""
+    g = syn.generate(900, 20, clade_size=10)
+    rng = np.random.default_rng(11)
+    pick = sorted(rng.choice(900, 61, replace=False).tolist())
+    if order == "shuffled":
+        rng.shuffle(pick)
+    ds = ParFAAIQSubData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"], g["genome_set"],
+                                    [g["genome_set"][i] for i in pick])
+    pb = ds.with_genome_major(g["G_off"], g["G_tet"]).problem()
+    engine.load(**pb)
+    others = [_capi.Engine(0), _capi.Engine(0)]
+    try:
+        for e in others:
+            e.load(**pb)
+        for flags in (0, _capi.FLAG_REF_COMPAT):
+            ref_a, ref_S, ref_N = engine.compute(flags)
+            n = len(ref_a)
+            a = np.full(n, np.nan)
+            S = np.full(n, np.nan)
+            N = np.full(n, -7, np.int32)
+            cuts = [0, 17, 40, 61]
+            for e, rb, re in zip([engine] + others, cuts[:-1], cuts[1:]):
+                e._check(e.lib.pfaai_compute_rows(e.ctx, rb, re, flags, a.ctypes.data, S.ctypes.data,
+                                                  N.ctypes.data), "pfaai_compute_rows")
+            assert np.array_equal(N, ref_N) and np.array_equal(S, ref_S) and np.array_equal(a, ref_a)
+    finally:
+        for e in others:
+            e.close()
 
 
 @pytest.mark.timeout(600)

@@ -60,8 +60,13 @@ def build_hip(force=False, diag=False):
     objs = [os.path.join(objdir, u[:-4] + ".o") for u in units]
     from concurrent.futures import ThreadPoolExecutor
 
-    with ThreadPoolExecutor(max_workers=min(len(units), int(os.environ.get("MAX_JOBS", "8")))) as ex:
-        futs = [ex.submit(_run, [HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)]) for u, o in zip(units, objs)]
+    # an object is rebuilt when its own unit or any shared header is newer
+    # (a row-kernel unit takes ~4 min: editing the C-ABI unit alone must not
+    # recompile them)
+    headers = [d for d in deps if not d.endswith(".hip")]
+    todo = [(u, o) for u, o in zip(units, objs) if force or _newer(o, [os.path.join(csrc, u), *headers])]
+    with ThreadPoolExecutor(max_workers=max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
+        futs = [ex.submit(_run, [HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)]) for u, o in todo]
         for f in futs:
             f.result()  # re-raises a failed compile
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs, "-ldl"])

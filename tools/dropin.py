@@ -74,7 +74,8 @@ def build(force=False):
     if not os.path.exists(main):
         return None
     lib = os.path.join(ROOT, "parfastaai_amd", "lib", "libpfaai_hip.so")
-    deps = [lib, os.path.join(ROOT, "include", "pfaai_hip.hpp"), os.path.join(ROOT, "INTEGRATION.md")]
+    deps = [lib, os.path.join(ROOT, "include", "pfaai_hip.hpp"), os.path.join(ROOT, "include", "pfaai_dropin.hpp"),
+            os.path.join(ROOT, "parfastaai_amd", "host", "scp_db.hpp"), os.path.join(ROOT, "INTEGRATION.md")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(d) <= os.path.getmtime(OUT) for d in deps):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round 6 GPU steps, one box, in the order given by STEPS (space separated):
+#   suite      the whole -m gpu suite
+#   tests      the tests named in TESTS (pytest node ids / files)
+#   qt         C4 shape: tools/gpu/qt_bench.py (50 000 targets x 1 000 queries)
+#   qt_r05     the same against round 5's library (tools/_build/ab, A/B)
+#   stream     C5 shape: tools/gpu/stream_bench.py, 100 000 genomes, no-op sink
+#   stream_r05 the same against round 5's library
+#   bench      the bench line (bench.py --steps 20 --warmup 5, no CPU baseline)
+#   smoke      __graft_entry__.smoke()
+# Every step has its own time limit and the first failure ends the call.
+#   TAG=r06a STEPS="tests qt qt_r05" TESTS=tests/test_gpu_stream.py bash tools/gpu/r06.sh
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/${TAG:-r06}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+R05=tools/_build/ab/libpfaai_hip_r05.so
+PYT="python3 -u -m pytest -x -v --timeout 500 --timeout-method thread -m gpu"
+for step in ${STEPS:-suite}; do
+  echo "== $step $(date +%T)"
+  case $step in
+    suite) timeout -k 10 1000 $PYT tests > "$OUT/tests.txt" 2>&1 || { tail -30 "$OUT/tests.txt"; exit 1; } ;;
+    tests) timeout -k 10 900 $PYT $TESTS > "$OUT/tests_sel.txt" 2>&1 || { tail -30 "$OUT/tests_sel.txt"; exit 1; } ;;
+    qt) timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4.json" 2> "$OUT/qt.err" || exit 1 ;;
+    qt_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4_r05.json" 2> "$OUT/qt_r05.err" || exit 1 ;;
+    stream) timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k.json" 2> "$OUT/stream.err" || exit 1 ;;
+    stream_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k_r05.json" 2> "$OUT/stream_r05.err" || exit 1 ;;
+    bench) timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline none > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1 ;;
+    smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  tail -c 600 "$OUT"/*.json 2>/dev/null | tail -3
+done
+echo "== done $(date +%T)"
