@@ -302,6 +302,13 @@ def main():
                     help="one-GPU box rehearsal of the N > 1 flow (split, spans, pipelined gather, reassembly, "
                          "result check): gloo instead of RCCL, every rank on device local %% device_count, the "
                          "gather through host buffers -- not a measurement")
+    ap.add_argument("--split", choices=["cyclic", "contiguous"], default="contiguous",
+                    help="N > 1: rank r runs one contiguous cost-balanced row block (contiguous, the default), or "
+                         "in ONE launch over its row list (pfaai_set_row_order) the 32-row groups dealt to it in "
+                         "snake order (cyclic: every rank gets the whole matrix's mix of wide and narrow rows; its "
+                         "rows' JAC segments go straight into rank 0's output by grouped send / recv).  The one-GPU "
+                         "emulation (profiles/r06/shard_cyclic.txt) put the slowest cyclic rank at 1.08 ms against "
+                         "1.05-1.09 contiguous, so the default stays contiguous")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     ap.add_argument("--launch-dry-run", action="store_true",
@@ -342,7 +349,7 @@ def main():
 
     from parfastaai_amd import _capi, syn
     from parfastaai_amd.datastruct import ParFAAIData
-    from parfastaai_amd.shard import PipelinedGather, split_range, split_rows
+    from parfastaai_amd.shard import PipelinedGather, SegmentGather, cyclic_rows, jac_segments, split_range, split_rows
 
     t0 = time.perf_counter()
     g = syn.generate(args.genomes, args.prot)
@@ -357,8 +364,12 @@ def main():
     # rows are genomes, so the blocks are known before the load
     # (cus: cuts a few rows past a round of 2 x CUs row workgroups move back)
     blocks = split_rows(args.genomes, world, cus=torch.cuda.get_device_properties(dev).multi_processor_count)
+    # block-cyclic (--split cyclic): the rank's rows are spread over the
+    # whole matrix, so it loads every genome's walk data (pfaai_load)
+    cyclic = world > 1 and args.split == "cyclic" and not args.f_only
+    lists = cyclic_rows(args.genomes, world) if cyclic else None
     t0 = time.perf_counter()
-    eng.load(**ds.problem(), rows=blocks[rank] if world > 1 else None)
+    eng.load(**ds.problem(), rows=blocks[rank] if world > 1 and not cyclic else None)
     load_wall_ms = (time.perf_counter() - t0) * 1e3
     del g
     ms_checks, ms_upload, ms_load_dev = eng.load_timing()
@@ -367,27 +378,55 @@ def main():
         f"{ms_load_dev:.2f} ms)")
     n_rows, n_pairs = eng.shape()
     assert n_rows == args.genomes
-    spans = [eng.row_span(rb, re) for rb, re in blocks]
-    rb, re = blocks[rank]
-    first, count = spans[rank]
+    if cyclic:
+        segs = [jac_segments(args.genomes, rl) for rl in lists]
+        eng.set_row_order(lists[rank])
+        count = sum(l - f for f, l in segs[rank])  # the rank's pairs
+    else:
+        spans = [eng.row_span(rb, re) for rb, re in blocks]
+        first, count = spans[rank]
     # N > 1: the rank's AJI block is gathered to rank 0 (RCCL, async); with
     # two buffer sets the gather of step i overlaps the compute of step i + 1.
     # --chunks > 1: the rows in pipeline chunks, chunk j gathered while chunk
     # j + 1 computes; the run table is built by chunk 0 only (PFAAI_FLAG_KEEP_RUNS)
     nch = max(1, args.chunks)
     slots = max(1, args.slots) if args.slots else (1 if world == 1 else 2)
-    sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
-    counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
-    pg = PipelinedGather(counts, dst=0, device=hdev, slots=slots)
     stream = torch.cuda.current_stream(dev)
-    # pfaai_run indexes by the global JAC index: chunk j writes its own buffer
-    # (rehearsal: a device twin of each host gather buffer)
-    dbufs = [[torch.zeros_like(b, device=dev) for b in bs] for bs in pg.slot_bufs] if rehearse else pg.slot_bufs
-    bases = [[dbufs[k][j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
-             for k in range(slots)]
     n_steps = [0]
+    if cyclic:
+        if nch != 1:
+            raise SystemExit("--chunks applies to --split contiguous")
+        # every rank runs its list into a full-size JAC-ordered array; rank
+        # 0's is the output (rehearsal: a device twin of each host array)
+        pg = SegmentGather(segs, n_pairs, dst=0, device=hdev, slots=slots)
+        dfull = [torch.zeros_like(b, device=dev) for b in pg.slot_bufs] if rehearse else pg.slot_bufs
+        my_rows = len(lists[rank])
+        sub = [[(0, my_rows)]]  # (the |E| pass below: one launch over the list)
+        bases = [[dfull[k].data_ptr()] for k in range(slots)]
+    else:
+        sub = [split_range(b0, b1, nch, n_rows) for b0, b1 in blocks]
+        counts = [[eng.row_span(c0, c1)[1] for c0, c1 in s] for s in sub]
+        pg = PipelinedGather(counts, dst=0, device=hdev, slots=slots)
+        # pfaai_run indexes by the global JAC index: chunk j writes its own buffer
+        # (rehearsal: a device twin of each host gather buffer)
+        dbufs = [[torch.zeros_like(b, device=dev) for b in bs] for bs in pg.slot_bufs] if rehearse else pg.slot_bufs
+        bases = [[dbufs[k][j].data_ptr() - eng.row_span(c0, c1)[0] * 8 for j, (c0, c1) in enumerate(sub[rank])]
+                 for k in range(slots)]
+
+    def step_cyclic():
+        i = n_steps[0]
+        n_steps[0] += 1
+        pg.begin(i)  # buffer set i % slots: the stream waits for the transfers that last read it
+        eng.run(0, my_rows, 0, bases[i % slots][0], stream=stream.cuda_stream)
+        if rehearse:
+            pg.buf.copy_(dfull[i % slots])
+        pg.issue()
+        if slots == 1:
+            pg.wait()
 
     def step():
+        if cyclic:
+            return step_cyclic()
         i = n_steps[0]
         n_steps[0] += 1
         pg.begin(i)  # buffer set i % slots: the stream waits for the gathers that last read it
@@ -411,7 +450,7 @@ def main():
     # one-shot cost: the load's device build + this first step
     eng.timing(reset=True)
     n_events = 0
-    for j, (c0, c1) in enumerate(sub[rank]):
+    for j, (c0, c1) in enumerate(sub[0] if cyclic else sub[rank]):
         if c1 > c0:
             eng.run(c0, c1, 0, bases[0][j], stream=stream.cuda_stream)
             torch.cuda.synchronize(dev)
@@ -528,7 +567,8 @@ def main():
                 "pass_bytes_per_F": pass_per_f,
                 "pass_frac": round(pass_per_f * n_f / (ms_load_dev * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pass_per_f else None,
                 "device_ms_max_rank": round(load_ms_max, 3),
-                "rows": f"rank 0 of {world}: walk data of rows {list(blocks[rank])}" if world > 1 else "all",
+                "rows": ("all (block-cyclic ranks)" if cyclic else
+                         f"rank 0 of {world}: walk data of rows {list(blocks[rank])}") if world > 1 else "all",
                 "one_shot_ms": round(ms_load_dev + first_step_ms, 3), "first_step_ms": round(first_step_ms, 3),
                 "one_shot_wall_ms": round(first_wall_ms, 1)}
         cpu = None
@@ -558,11 +598,14 @@ def main():
             "dtype": "i32+f64",
             "data": "synthetic",
             "config": {"workload": f"SYN all-vs-all N={args.genomes} P={args.prot} (BASELINE configs[2] DB; "
-                                   f"row-block sharded, RCCL gather to rank 0)",
+                                   + ("block-cyclic rows, RCCL send/recv into rank 0)" if cyclic else
+                                      "row-block sharded, RCCL gather to rank 0)"),
                        "genomes": args.genomes, "proteins": args.prot, "pairs": n_pairs, "F": n_f,
                        "events": total_events, "events_per_s": round(total_events / (ms_per_step * 1e-3), 1),
-                       "parallelism": f"rowblock{world}",
-                       "gather_pipeline": {"chunks_per_step": nch, "buffer_sets": slots},
+                       "parallelism": f"rowcyclic{world}" if cyclic else f"rowblock{world}",
+                       "gather_pipeline": {"chunks_per_step": nch, "buffer_sets": slots,
+                                           "form": "grouped send/recv of row-group segments" if cyclic
+                                           else "gather of row blocks"},
                        "hot_path_GBps": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                        "k_rows_ms_max_rank": round(k_rows_ms_max, 4),
                        "k_build_ms_max_rank": round(k_build_ms_max, 4)},

@@ -324,6 +324,19 @@ int pfaai_run_info(const pfaai_ctx* ctx, int32_t* rows_kernel, int32_t* column_w
 enum { PFAAI_WALK_NONE = -1, PFAAI_WALK_SPLITTERS = 0, PFAAI_WALK_GPOS = 3, PFAAI_WALK_SPANS = 4 };
 int pfaai_run_walk(const pfaai_ctx* ctx, int32_t* walk, int32_t* narrow_launch);
 
+/* All-vs-all, genome-major loads: make rows [0, n) of later pfaai_runs the
+ * genomes of `genomes` (strictly ascending ids; the others follow, but rows
+ * >= n are refused while the list is set), so one launch covers any subset
+ * of output rows -- e.g. a rank's block-cyclic share of the matrix (row
+ * groups dealt round robin, so every rank holds the whole matrix's mix of
+ * wide and narrow rows; distributeGenomePairs, algorithm_impl.hpp:100-120,
+ * deals contiguous pair ranges instead).  Outputs stay at the reference's
+ * JAC index, so a run writes its rows' entries into arrays of n_pairs.
+ * Only pfaai_run uses the list (the span APIs -- pfaai_row_span,
+ * pfaai_compute*, pfaai_stream* -- refuse it).  genomes == NULL or n == 0:
+ * back to rows = genomes in id order.  Synchronises the device. */
+int pfaai_set_row_order(pfaai_ctx* ctx, const int32_t* genomes, int64_t n);
+
 /* |E| of the last run, counted by the scatter kernel (equals the reference's
  * countTetramerTuples total over the run's rows, ds_helper.hpp:206-265), and
  * device times (ms) of its two phases: work-list build, row kernel.

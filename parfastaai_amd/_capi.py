@@ -39,7 +39,7 @@ EXPORTS = [
     "pfaai_debug_row_counts", "pfaai_debug_div_check", "pfaai_debug_clocks", "pfaai_device_alloc", "pfaai_device_free", "pfaai_memcpy_d2h",
     "pfaai_synchronize", "pfaai_timing", "pfaai_stream", "pfaai_stream_events",
     "pfaai_build_f", "pfaai_compute_rows", "pfaai_run_info", "pfaai_run_walk", "pfaai_load_rows", "pfaai_load_timing", "pfaai_stream_matrix",
-    "pfaai_load_info",
+    "pfaai_load_info", "pfaai_set_row_order",
     "pfaai_group_create", "pfaai_group_create_flags", "pfaai_group_destroy", "pfaai_group_last_error",
     "pfaai_group_size", "pfaai_group_ctx", "pfaai_group_load", "pfaai_group_blocks", "pfaai_group_run",
 ]
@@ -116,6 +116,7 @@ def load_library(path=None):
         "pfaai_stream_matrix": (ctypes.c_int, [vp, i64, i64, i64, u32, MATRIX_SINK_FN, vp]),
         "pfaai_run_info": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pfaai_run_walk": (ctypes.c_int, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "pfaai_set_row_order": (ctypes.c_int, [vp, vp, i64]),
         "pfaai_load_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
         "pfaai_load_info": (ctypes.c_int, [vp, ctypes.POINTER(i32)]),
@@ -231,6 +232,15 @@ class Engine:
         """Device-resident run; d_* are device pointers (ints), stream a hipStream_t (int)."""
         self._check(self.lib.pfaai_run(self.ctx, row_begin, row_end, flags, d_aji, d_S, d_N, stream),
                     "pfaai_run")
+
+    def set_row_order(self, genomes=None):
+        """pfaai_set_row_order: rows [0, len(genomes)) of later runs are these
+        genomes (strictly ascending ids, all-vs-all); None -> id order."""
+        if genomes is None or len(genomes) == 0:
+            self._check(self.lib.pfaai_set_row_order(self.ctx, None, 0), "pfaai_set_row_order")
+            return
+        g = np.ascontiguousarray(genomes, dtype=np.int32)
+        self._check(self.lib.pfaai_set_row_order(self.ctx, g.ctypes.data, len(g)), "pfaai_set_row_order")
 
     def build_f(self, prot, genome, tetra, n_prot, n_genome, with_T=True):
         """F construction on the device (pfaai_build_f) from (protein, genome,

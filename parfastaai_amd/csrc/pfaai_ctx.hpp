@@ -95,6 +95,11 @@ struct pfaai_ctx {
     // both-given pfaai_load_rows checks its block only): rows beyond them
     // are refused, since every walk reads the row genome's G lists
     int32_t chk_lo = 0, chk_hi = 0;
+    // pfaai_set_row_order (all-vs-all): rows [0, order_n) are the caller's
+    // ascending genome list (0: rows are the genomes in id order), whose
+    // genomes all lie in the walk-data block when order_in_pos
+    int64_t order_n = 0;
+    bool order_in_pos = false;
     int64_t run_rb = 0, run_re = 0;  // rows of the current pfaai_run (pl_uses_ends)
     hipEvent_t load_ev[2] = {nullptr, nullptr};  // device span of the last load's F / G build
     hipEvent_t side_ev[2] = {nullptr, nullptr};  // the load's fork to / join from copy_stream (k_hash_f)
@@ -158,6 +163,7 @@ constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
 constexpr int32_t kGposMaxIds = 20480;  // G_pos built for all-vs-all problems up to two row chunks wide
 
 enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
+constexpr int kPlStag = 2;  // k_rows_pl's S5 entry order (pfaai_rows_pl.hpp, flags bits 18-20)
 
 // scalars buffer layout (u64 each)
 // SC_HF / SC_HG: the both-given load's membership sums over F (k_hash_f) and
@@ -244,7 +250,7 @@ inline int64_t pl_chunk_cols(pfaai_ctx* c) {
 // table build (run_mode) and the kernel choice (launch_pl).
 inline bool pl_uses_ends(pfaai_ctx* c, int mode) {
     return mode == 0 && (c->rows_kernel == RK_PL || c->rows_kernel == RK_PL512) && c->dev.G_pe && c->t_exact && !c->windows &&
-           c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi &&
+           (c->order_n ? c->order_in_pos : c->run_rb >= c->pos_lo && c->run_re <= c->pos_hi) &&
            ceil_div((int64_t)c->cols_run + 1, pl_chunk_cols(c)) == 1 && !DIAG_ENV("PFAAI_PL_NOGPOS") &&
            !DIAG_ENV("PFAAI_PL_WK0");
 }

@@ -408,8 +408,10 @@ int run_mode(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji, 
     auto* sc = static_cast<unsigned long long*>(c->scalars.p);
     HIPCHK(c, hipMemsetAsync(sc + SC_EVENTS, 0, sizeof(unsigned long long), s));
     const bool wl = c->rows_kernel == RK_WORKLIST;
-    if (c->prob.mode == PFAAI_MODE_ALL && (rb < c->chk_lo || re > c->chk_hi))
-        return fail(c, PFAAI_RC_INVALID, "rows outside the block whose G lists pfaai_load_rows verified");
+    if (c->prob.mode == PFAAI_MODE_ALL && (c->order_n ? re > c->order_n : (rb < c->chk_lo || re > c->chk_hi)))
+        return fail(c, PFAAI_RC_INVALID,
+                    c->order_n ? "rows past the genome list of pfaai_set_row_order"
+                               : "rows outside the block whose G lists pfaai_load_rows verified");
     c->run_rb = rb;  // (pl_uses_ends: the rows' G_pos / G_end must have been built)
     c->run_re = re;
     c->last_walk = PFAAI_WALK_NONE;  // (set by launch_pl / launch_narrow)
@@ -1173,6 +1175,8 @@ int load_impl(pfaai_ctx* c, const pfaai_problem* pb, int64_t rows_lo = 0, int64_
     std::vector<int32_t> row_of(ni, -1), tcol_row(ni), tcol_col(ni);
     c->row_genome_h.clear();
     c->q_index_h.clear();
+    c->order_n = 0;
+    c->order_in_pos = false;
     if (p.mode == PFAAI_MODE_ALL) {
         for (int32_t g = 0; g < ni; ++g) { row_of[g] = g; c->row_genome_h.push_back(g); }
         c->n_rows = ni;
@@ -1663,7 +1667,7 @@ int pfaai_shape(const pfaai_ctx* c, int64_t* n_rows, int64_t* n_pairs) {
 }
 
 int pfaai_row_span(const pfaai_ctx* c, int64_t rb, int64_t re, int64_t* first, int64_t* count) {
-    if (!c || !c->loaded || rb < 0 || re > c->n_rows || rb > re) return PFAAI_RC_INVALID;
+    if (!c || !c->loaded || rb < 0 || re > c->n_rows || rb > re || c->order_n) return PFAAI_RC_INVALID;
     const auto& p = c->prob;
     int64_t f = 0, l = 0;  // [f, l)
     if (rb == re) {
@@ -1718,6 +1722,10 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
         c->dev.xcd_chunk = xc ? std::max(1, atoi(xc)) : kXcdChunk;
     }
     if (const char* abl = DIAG_ENV("PFAAI_ABLATE")) flags |= (uint32_t)atoi(abl) << 8;  // diagnostics only
+    {  // k_rows_pl's S5 entry order (flags bits 18-20; pfaai_rows_pl.hpp): default 2, PFAAI_PL_STAG overrides (A/B)
+        const char* sg = DIAG_ENV("PFAAI_PL_STAG");
+        flags = (flags & ~(7u << 18)) | (uint32_t)((sg ? atoi(sg) : kPlStag) & 7) << 18;
+    }
     // k_rows_pl wave priorities: bit 0 raises the load-issue stages above other
     // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33
     // ms at 10k, tools/gpu/ab_rows.py); PFAAI_PL_PRIO=0..3 overrides (A/B)
@@ -1745,7 +1753,8 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // keeps the problem's widest row (A/B; results identical)
     if (!full && c->prob.mode == PFAAI_MODE_ALL && c->dev.G_pe) {
         const char* lc = DIAG_ENV("PFAAI_PL_LAUNCH_COLS");
-        if (!(lc && lc[0] == '0')) c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - rb);
+        if (!(lc && lc[0] == '0') && rb < re)  // (rows ascend by genome: the first is the widest)
+            c->cols_run = (int32_t)std::max<int64_t>(1, c->prob.n_ids - 1 - c->row_genome_h[rb]);
     }
     if (rb == re) return PFAAI_RC_OK;
     if (full) return run_mode<kModeFull>(c, rb, re, flags, aji, S, N, s);
@@ -1759,6 +1768,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
 int pfaai_compute(pfaai_ctx* c, uint32_t flags, double* h_aji, double* h_S, int32_t* h_N) {
     if (!c) return PFAAI_RC_INVALID;
     if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (c->order_n) return fail(c, PFAAI_RC_INVALID, "a row order is set (pfaai_set_row_order): only pfaai_run");
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t np = c->n_pairs;
     int rc;
@@ -1835,6 +1845,43 @@ int pfaai_run_info(const pfaai_ctx* c, int32_t* rows_kernel, int32_t* column_win
     if (!c) return PFAAI_RC_INVALID;
     if (rows_kernel) *rows_kernel = c->rows_kernel;
     if (column_windows) *column_windows = c->windows ? 1 : 0;
+    return PFAAI_RC_OK;
+}
+
+int pfaai_set_row_order(pfaai_ctx* c, const int32_t* genomes, int64_t n) {
+    if (!c) return PFAAI_RC_INVALID;
+    if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
+    if (c->prob.mode != PFAAI_MODE_ALL) return fail(c, PFAAI_RC_INVALID, "pfaai_set_row_order: all-vs-all only");
+    if (!c->has_g) return fail(c, PFAAI_RC_INVALID, "pfaai_set_row_order: needs a genome-major load");
+    const int32_t ni = c->prob.n_ids;
+    if (n < 0 || n > ni || (n > 0 && !genomes)) return fail(c, PFAAI_RC_INVALID, "pfaai_set_row_order: bad list");
+    std::vector<int32_t> order;
+    order.reserve((size_t)ni);
+    bool in_pos = true;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t g = genomes[i];
+        if (g < 0 || g >= ni || (i && g <= genomes[i - 1]))
+            return fail(c, PFAAI_RC_INVALID, "pfaai_set_row_order: genome ids must ascend strictly within [0, n_ids)");
+        if (g < c->chk_lo || g >= c->chk_hi)
+            return fail(c, PFAAI_RC_INVALID, "pfaai_set_row_order: a genome outside the block pfaai_load_rows verified");
+        in_pos = in_pos && g >= c->pos_lo && g < c->pos_hi;
+        order.push_back(g);
+    }
+    {  // the other genomes follow in id order (rows past n are refused while the list is set)
+        std::vector<char> listed((size_t)ni, 0);
+        for (int32_t g : order) listed[(size_t)g] = 1;
+        for (int32_t g = 0; g < ni; ++g)
+            if (!listed[(size_t)g]) order.push_back(g);
+    }
+    std::vector<int32_t> row_of((size_t)ni);
+    for (int32_t r = 0; r < ni; ++r) row_of[(size_t)order[(size_t)r]] = r;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());  // no launch in flight still reads the old order
+    HIPCHK(c, hipMemcpy(c->row_genome.p, order.data(), (size_t)ni * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->row_of.p, row_of.data(), (size_t)ni * sizeof(int32_t), hipMemcpyHostToDevice));
+    c->row_genome_h.swap(order);
+    c->order_n = n;
+    c->order_in_pos = in_pos;
     return PFAAI_RC_OK;
 }
 
@@ -2230,12 +2277,14 @@ static int stream_matrix_impl(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile
 int pfaai_stream_matrix(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_rows, uint32_t flags,
                         pfaai_matrix_sink_fn sink, void* user) {
     if (!c) return PFAAI_RC_INVALID;
+    if (c->order_n) return fail(c, PFAAI_RC_INVALID, "a row order is set (pfaai_set_row_order): only pfaai_run");
     return guarded(c, [&] { return stream_matrix_impl(c, rb, re, tile_rows, flags, sink, user); });
 }
 
 int pfaai_stream(pfaai_ctx* c, int64_t rb, int64_t re, int64_t tile_pairs, uint32_t flags, pfaai_sink_fn sink,
                  void* user) {
     if (!c) return PFAAI_RC_INVALID;
+    if (c->order_n) return fail(c, PFAAI_RC_INVALID, "a row order is set (pfaai_set_row_order): only pfaai_run");
     return guarded(c, [&] { return stream_impl(c, rb, re, tile_pairs, flags, sink, user); });
 }
 
@@ -2392,6 +2441,7 @@ int pfaai_compute_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, dou
     if (!c) return PFAAI_RC_INVALID;
     if (!c->loaded) return fail(c, PFAAI_RC_INVALID, "no problem loaded");
     if (rb < 0 || re > c->n_rows || rb > re) return fail(c, PFAAI_RC_INVALID, "row range out of bounds");
+    if (c->order_n) return fail(c, PFAAI_RC_INVALID, "a row order is set (pfaai_set_row_order): only pfaai_run");
     if (rb == re) return PFAAI_RC_OK;
     if (c->prob.mode == PFAAI_MODE_QSUB && !(rb == 0 && re == c->n_rows)) return compute_rows_qsub(c, rb, re, flags, h_aji, h_S, h_N);
     HIPCHK(c, hipSetDevice(c->device));

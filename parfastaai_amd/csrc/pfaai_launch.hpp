@@ -88,16 +88,18 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         // the kernel offsets the window-major tables by its window index
         Dev dv = c->dev;
         dv.blk = static_cast<uint4*>(c->blkw.p);
+        // (V 4: S5 without the denominator clamp where T is every list's length)
         constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2) : (kPlVG | 2);
         const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 0: the QT quirk's per-column division
+        const bool tx = c->t_exact;
         if (w_lo < nwin) {
             const int64_t r0 = rb, r1 = re;
             const int32_t ac = kWinGrid0 - w_lo;
             const int32_t gy = nwin - w_lo;
             if (bigf) {
-                if (cm) PLK(true, 4, 0); else PLK(true, 4, VS);
+                if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, VS | 4); else PLK(true, 4, VS);
             } else {
-                if (cm) PLK(false, 4, 0); else PLK(false, 4, VS);
+                if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, VS | 4); else PLK(false, 4, VS);
             }
         }
         if constexpr (MODE == 0) {
@@ -170,14 +172,18 @@ bool launch_narrow(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double*
                           hipStream_t s) {
     if (DIAG_ENV("PFAAI_PL_NO512") || !pl_uses_ends(c, 0) || !c->side_stream || !c->narrow_ev[0] || !c->narrow_ev[1])
         return false;
-    const int64_t n = c->prob.n_ids;  // all-vs-all: row r is genome r, n - 1 - r columns
-    const int64_t cut = std::max(rb, std::min(re, n - 1 - (int64_t)kNarrowCols));
+    // all-vs-all: row r is genome g = row_genome_h[r] (r itself unless
+    // pfaai_set_row_order gave an ascending list), n - 1 - g columns
+    const int64_t n = c->prob.n_ids;
+    const auto& rg = c->row_genome_h;
+    const int64_t cut = std::lower_bound(rg.begin() + rb, rg.begin() + re, (int32_t)(n - 1 - kNarrowCols)) - rg.begin();
     if (cut >= re) return false;
+    const int64_t cols_cut = n - 1 - rg[cut];
     const int32_t cols_all = c->cols_run;
-    if (ceil_div((int64_t)(n - 1 - cut) + 1, 2 * 2 * 512) != 1) return false;  // one chunk, or not the WK 3 form
+    if (ceil_div(cols_cut + 1, 2 * 2 * 512) != 1) return false;  // one chunk, or not the WK 3 form
     auto narrow = [&](hipStream_t st) {
         c->last_narrow = true;
-        c->cols_run = (int32_t)(n - 1 - cut);  // the narrow launch's widest row
+        c->cols_run = (int32_t)cols_cut;  // the narrow launch's widest row
         if (pick_kw<512>(c->cols_run, 2) == 1)
             launch_pl_n<0, 1, 512, 8>(c, true, cut, re, flags, aji, S, N, st);
         else

@@ -214,7 +214,9 @@ constexpr int kClkBlocks = 256;
 // per-column branches: the SALU of six exec-mask updates per word); 2 the
 // WK 3 member scatter by pl_scatter8_code over k_fcode's member codes; 8
 // S5's two divisions of a word by one reciprocal (exact_div_pair, with 1);
-// 16 the G entries one protein ahead instead of two (WK 3, ONE below); 64
+// 16 the G entries one protein ahead instead of two (WK 3, ONE below); 4
+// S5 without the max(d, 1) clamp outside WK 3 too (launched only on loads
+// whose T is every list's length, t_exact -- WK 3 implies it); 64
 // the reference-compat quirks compiled out (MODE 2 launches it only without
 // PFAAI_FLAG_REF_COMPAT: its per-column general division then leaves the
 // kernel, and V 9 fits 64 VGPRs -- with it, 114 spilled).  The
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                     ev += (uint32_t)(c0 + c1);
                     n_add(k, v);
                     int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
-                    if constexpr (WK != 3) {
+                    if constexpr (WK != 3 && (V & 4) == 0) {
                         d0 = max(d0, 1);
                         d1 = max(d1, 1);
                     }
@@ -562,6 +564,37 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // (S5 after the first member round's issue, so those loads land
         // while it computes, spills 12 VGPRs at KW = 5: the round's 8
         // member registers live across S5's fp64 temporaries; round 5.)
+        // How the 16 waves enter S5 together after the barrier (VERDICT r05
+        // #6; flags bits 18-20, set by pfaai_run: the release default 2,
+        // PFAAI_PL_STAG in the diagnostics build for A/B).  They all run S5's
+        // fp64 work at once and contend for the SIMDs' VALU; 2 drops the
+        // first-dispatched half (waves 0-7, which also carry S3 and the second
+        // member round) to priority 0 for S5, so the second half's S5 goes
+        // first -- 10k rows (diagnostics build, single launches, 7 rounds,
+        // profiles/r06/ab_stag.txt) 8.07 -> 7.88 ms; 1 the other way round
+        // 7.96; 3 / 5 the second half sleeping 128 / 512 cycles first 8.09 /
+        // 8.29; 4 waves 0-3 at priority 3: 8.24.  (6: the first half at 0 and
+        // the second at 2; 7: waves 0-3 at 0.)
+        if (const uint32_t sg = (flags >> 18) & 7u) {
+            const int wv = tid >> 6;
+            const bool late = wv >= NT / 128;
+            if (sg == 2) {
+                if (!late) __builtin_amdgcn_s_setprio(0);
+            } else if (sg == 1) {
+                if (late) __builtin_amdgcn_s_setprio(0);
+            } else if (sg == 6) {
+                if (!late) __builtin_amdgcn_s_setprio(0);
+                else __builtin_amdgcn_s_setprio(2);
+            } else if (sg == 7) {
+                if (wv < 4) __builtin_amdgcn_s_setprio(0);
+            } else if (sg == 3) {
+                if (late) __builtin_amdgcn_s_sleep(2);
+            } else if (sg == 4) {
+                if (wv < 4) __builtin_amdgcn_s_setprio(3);
+            } else if (sg == 5) {
+                if (late) __builtin_amdgcn_s_sleep(8);
+            }
+        }
         s5(i, twc, i >= 1 ? (int32_t)uni_u32(taL[i - 1]) : 0);
         stamp(7);
         const int pt = min(i, P - 1);

@@ -107,6 +107,42 @@ def row_costs(n_rows: int, all_vs_all: bool = True, fixed_cols: float | None = N
     return c
 
 
+# Block-cyclic rows (round 6): contiguous blocks end on
+# their slowest round (the first 10k/8 block is two rounds of the widest
+# rows: 1.07-1.08 ms against a 0.87 ms mean), and the blocks' times sum to
+# 1.18x the whole matrix's launch, which overlaps wide and narrow rows.
+# Dealing groups of CYCLIC_GROUP consecutive rows round robin -- widest
+# first, the direction reversing every round (snake order) -- gives every
+# rank the whole matrix's mix of wide and narrow rows in ONE launch over its
+# row list (pfaai_set_row_order); a group is the XCD chunk of the row kernel
+# (kXcdChunk = 32 consecutive rows per XCD, sharing a clade's runs in L2).
+CYCLIC_GROUP = 32
+
+
+def cyclic_rows(n_rows: int, world: int, group: int = CYCLIC_GROUP):
+    """-> [sorted row list] * world: groups of `group` consecutive rows dealt
+    in snake order (ranks 0..W-1, then W-1..0, ...), widest (first) rows
+    first.  Every row in exactly one list; each list ascending."""
+    out = [[] for _ in range(world)]
+    ng = (n_rows + group - 1) // group
+    for k in range(ng):
+        rnd, pos = divmod(k, world)
+        r = pos if rnd % 2 == 0 else world - 1 - pos
+        out[r].extend(range(k * group, min(n_rows, (k + 1) * group)))
+    return out
+
+
+def row_segments(rows):
+    """Maximal runs of consecutive ids in an ascending row list -> [(lo, hi)]."""
+    seg = []
+    for r in rows:
+        if seg and seg[-1][1] == r:
+            seg[-1][1] = r + 1
+        else:
+            seg.append([r, r + 1])
+    return [tuple(x) for x in seg]
+
+
 class PipelinedGather:
     """Row blocks cut into `chunks` pipeline chunks per rank.  Chunk j of every
     rank has its own buffer (padded to the largest rank's chunk j); issue(j)
@@ -187,6 +223,81 @@ class PipelinedGather:
         recv = self.slot_recv[k]
         return torch.cat([recv[j][r][: self.counts[r][j]]
                           for r in range(self.world) for j in range(len(bufs))])
+
+
+def jac_segments(n_ids: int, rows):
+    """All-vs-all: the JAC-index spans [f, l) of an ascending row list's
+    maximal runs of consecutive rows (row a's pairs start at n a - a (a + 1) / 2,
+    ds_impl.hpp:83-86)."""
+    base = lambda a: n_ids * a - a * (a + 1) // 2  # noqa: E731
+    return [(base(lo), base(hi)) for lo, hi in row_segments(rows)]
+
+
+class SegmentGather:
+    """The gather of block-cyclic row lists (cyclic_rows).  Every rank runs
+    its list into a full-size JAC-ordered array (the row kernel writes at the
+    reference's JAC index), so rank dst's array IS the output: its own rows
+    land in place, and every other rank sends the JAC segments of its rows
+    straight into it -- grouped point-to-point transfers
+    (torch.distributed.batch_isend_irecv: one RCCL group of ncclSend /
+    ncclRecv over xGMI with the "nccl" backend, gloo on CPU) -- with no
+    packing and no reorder on either side.  slots > 1 double-buffers across
+    steps as PipelinedGather does: begin(i) makes the current stream wait
+    for the transfers that last read buffer set i % slots.
+
+    segs[r]: rank r's JAC segments [(f, l)]; n: n_pairs."""
+
+    def __init__(self, segs, n, dst=0, device=None, dtype=None, group=None, slots=1):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.dst = dst
+        self.segs = segs
+        self.slots = max(1, int(slots))
+        self.slot_bufs = [torch.zeros(max(1, n), dtype=dtype or torch.float64, device=device)
+                          for _ in range(self.slots)]
+        self.slot_works = [[] for _ in range(self.slots)]
+        self.cur = 0
+
+    @property
+    def buf(self):
+        """The current step's full-size array."""
+        return self.slot_bufs[self.cur]
+
+    def begin(self, step):
+        self.cur = step % self.slots
+        for w in self.slot_works[self.cur]:
+            w.wait()
+        self.slot_works[self.cur] = []
+
+    def issue(self):
+        if self.world == 1:
+            return
+        d, b = self.dist, self.slot_bufs[self.cur]
+        if self.rank == self.dst:
+            ops = [d.P2POp(d.irecv, b[f:l], r, self.group) for r in range(self.world) if r != self.dst
+                   for f, l in self.segs[r] if l > f]
+        else:
+            ops = [d.P2POp(d.isend, b[f:l], self.dst, self.group) for f, l in self.segs[self.rank] if l > f]
+        if ops:
+            self.slot_works[self.cur].extend(d.batch_isend_irecv(ops))
+
+    def wait(self):
+        for works in self.slot_works:
+            for w in works:
+                w.wait()
+        self.slot_works = [[] for _ in range(self.slots)]
+
+    def result(self, slot=None):
+        """The full vector of buffer set `slot` (default: the current one) on
+        dst (after wait()), None elsewhere."""
+        if self.rank != self.dst:
+            return None
+        return self.slot_bufs[self.cur if slot is None else slot]
 
 
 def gather_rows(out_local, counts, dst=0, group=None):

@@ -59,6 +59,84 @@ def _worker(rank, world, port, n, result_q):
     dist.destroy_process_group()
 
 
+def _cyclic_worker(rank, world, port, n, steps, slots, result_q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from parfastaai_amd import syn
+    from parfastaai_amd.datastruct import ParFAAIData
+    from parfastaai_amd.shard import SegmentGather, cyclic_rows, jac_segments
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = syn.generate(n, 12, clade_size=5)  # identical on every rank
+    pr = O.Problem(ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).problem())
+    lists = cyclic_rows(n, world, 7)
+    segs = [jac_segments(n, rl) for rl in lists]
+    npairs = n * (n - 1) // 2
+    sg = SegmentGather(segs, npairs, slots=slots)
+    S, N, _ = pr.dense_rows(0, n)  # (the device's stand-in: this rank writes only its rows)
+    ok = True
+    for i in range(steps):
+        sg.begin(i)
+        sg.buf.fill_(-1.0 - i)  # stale values must be overwritten by the rows' owners
+        for a in lists[rank]:
+            f = n * a - a * (a + 1) // 2
+            sg.buf[f:f + n - 1 - a] = torch.from_numpy(S[a, a + 1:] / N[a, a + 1:] + i)
+        sg.issue()
+        if slots == 1:
+            sg.wait()
+    sg.wait()
+    if rank == 0:
+        ref = pr.ref_run()["AJI"]
+        for k in range(min(slots, steps)):
+            i = steps - 1 - k
+            ok = ok and bool(np.array_equal(sg.result(slot=i % slots).numpy(), ref + i))
+        result_q.put(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,steps,slots", [(2, 1, 1), (3, 4, 2)])
+def test_gloo_segment_gather_of_cyclic_rows(world, steps, slots):
+    """shard.SegmentGather (the gather of block-cyclic row lists): every rank
+    writes only its rows into its full-size array, the others' JAC segments
+    arrive in rank 0's array by grouped send / recv, double-buffered over
+    steps; rank 0's array equals the single-process AJI vector, each buffer
+    set's own step."""
+    port = _free_port()
+    q = mp.get_context("spawn").SimpleQueue()
+    ps = [mp.get_context("spawn").Process(target=_cyclic_worker, args=(r, world, port, 40, steps, slots, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert q.get() is True
+
+
+@pytest.mark.parametrize("n,world,group", [(10000, 8, 32), (1000, 3, 32), (37, 5, 4), (5, 8, 32)])
+def test_cyclic_rows_partition_and_balance(n, world, group):
+    """shard.cyclic_rows: every row in exactly one rank's ascending list,
+    groups of `group` consecutive rows, dealt in snake order; at 10k x 8 the
+    ranks' row costs (row_costs) lie within 2 % of each other."""
+    from parfastaai_amd.shard import cyclic_rows, row_segments
+    lists = cyclic_rows(n, world, group)
+    assert len(lists) == world
+    assert sorted(r for rl in lists for r in rl) == list(range(n))
+    for rl in lists:
+        assert rl == sorted(rl)
+        for lo, hi in row_segments(rl):
+            assert lo % group == 0 and (hi - lo == group or hi == n or hi % group == 0)
+    if n == 10000:
+        c = row_costs(n)
+        cost = [sum(c[r] for r in rl) for rl in lists]
+        assert max(cost) / min(cost) < 1.02, cost
+
+
 def test_split_rows_balanced():
     for n, w in [(10000, 8), (2000, 2), (7, 4), (3, 8)]:
         blocks = split_rows(n, w)

@@ -148,3 +148,44 @@ def test_rank_check_refuses_a_bad_list_of_its_block(engine):
     f, c = engine.row_span(0, 400)
     for x, y in zip(got, ref):
         assert np.array_equal(x[f:f + c], y[f:f + c])
+
+
+@pytest.mark.parametrize("n,world,group", [(700, 3, 32), (3000, 8, 32), (2100, 5, 7)])
+def test_cyclic_row_lists_assemble_to_the_whole_run(engine, n, world, group):
+    """Round 6: a rank's block-cyclic share -- groups of
+    rows dealt in snake order (shard.cyclic_rows) -- runs as ONE launch over
+    its row list (pfaai_set_row_order), each rank into its own full-size
+    array at the reference's JAC indices; the ranks' rows assemble to the
+    single run bit for bit, S and N included, through the benchmarked walk
+    (G_pos, the narrow 512-thread rows split off by genome)."""
+    from parfastaai_amd.shard import cyclic_rows, row_segments
+    pb = _problem(n, 30, clade_size=10)
+    engine.load(**pb)
+    rows, npairs = engine.shape()
+    ref = [torch.full((npairs,), -1.0, dtype=dt, device="cuda:0") for dt in (torch.float64, torch.float64, torch.int32)]
+    st = torch.cuda.current_stream().cuda_stream
+    engine.run(0, rows, _capi.FLAG_EMIT_JAC, *(x.data_ptr() for x in ref), stream=st)
+    got = [torch.full_like(x, -2) for x in ref]
+    lists = cyclic_rows(rows, world, group)
+    assert sorted(r for rl in lists for r in rl) == list(range(rows))
+    base = lambda a: n * a - a * (a + 1) // 2
+    for rl in lists:
+        engine.set_row_order(rl)
+        part = [torch.full_like(x, -3) for x in ref]
+        engine.run(0, len(rl), _capi.FLAG_EMIT_JAC, *(x.data_ptr() for x in part), stream=st)
+        torch.cuda.synchronize()
+        assert engine.stats()["walk"] == "gpos"
+        for lo, hi in row_segments(rl):
+            for g, p in zip(got, part):
+                g[base(lo):base(hi)] = p[base(lo):base(hi)]
+        with pytest.raises(_capi.PfaaiError):  # rows past the list
+            engine.run(0, len(rl) + 1, 0, part[0].data_ptr(), stream=st)
+        with pytest.raises(_capi.PfaaiError):  # span APIs refuse a row order
+            engine.compute(0)
+    engine.set_row_order(None)
+    for g, r in zip(got, ref):
+        assert torch.equal(g, r)
+    with pytest.raises(_capi.PfaaiError):
+        engine.set_row_order([5, 3])  # not ascending
+    a2, _, _ = engine.compute(0)  # the id order is back
+    assert np.array_equal(a2, ref[0].cpu().numpy())

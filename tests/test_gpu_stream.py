@@ -271,8 +271,11 @@ def test_compute_rows_qsub_blocks_fill_one_array(engine, order):
     each block's cross cells by span, its query-query cells merged into the
     triangle cell by cell -- fill one array equal to pfaai_compute, for a
     query list in DB order and one shuffled (a pair's cell
-    then lies in another block's rows), ref-compat included; three contexts
-    on device 0 as in the CLI's --devices 0,0,0."""
+    then lies in another block's rows), ref-compat included for the sorted
+    list (with a shuffled one the reference's unswapped triangle index makes
+    pairs collide on one cell, ds_impl.hpp:257-262: undefined there, single
+    device included); three contexts on device 0 as in the CLI's --devices
+    0,0,0."""
     g = syn.generate(900, 20, clade_size=10)
     rng = np.random.default_rng(11)
     pick = sorted(rng.choice(900, 61, replace=False).tolist())
@@ -286,7 +289,7 @@ def test_compute_rows_qsub_blocks_fill_one_array(engine, order):
     try:
         for e in others:
             e.load(**pb)
-        for flags in (0, _capi.FLAG_REF_COMPAT):
+        for flags in (0, _capi.FLAG_REF_COMPAT) if order == "sorted" else (0,):
             ref_a, ref_S, ref_N = engine.compute(flags)
             n = len(ref_a)
             a = np.full(n, np.nan)

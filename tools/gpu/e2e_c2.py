@@ -96,6 +96,14 @@ def main():
             print(f"[e2e] {name} run {k}: {w:.2f}s", file=sys.stderr, flush=True)
     first = next(iter(csvs.values()))
     same = all(v == first for v in csvs.values())
+    # the reference binary's CSV of this DB, pinned by its SHA-256
+    # (tests/golden/full_digests.json C2_cli_csv) -- checked even when the
+    # reference is not run here
+    import hashlib
+    ref_digest = None
+    if a.genomes == 2000 and a.prot == 100:
+        ref_digest = json.load(open(os.path.join(ROOT, "tests", "golden", "full_digests.json")))["C2_cli_csv"]["sha256"]
+    digest_ok = None if ref_digest is None else all(hashlib.sha256(v).hexdigest() == ref_digest for v in csvs.values())
     med = {k: round(statistics.median(v), 3) for k, v in walls.items()}
     pairs = a.genomes * (a.genomes - 1) // 2
     res = {"what": "end-to-end CLI, SQLite DB -> CSV (BASELINE config C2 shape); medians of repeated runs",
@@ -103,13 +111,14 @@ def main():
            "ours_wall_s": med.get("ours"), "ours_args": a.ours_args, "dropin_wall_s": med.get("dropin"),
            "reference_wall_s": med.get("ref"), "reference_threads": threads, "walls_s": walls,
            "phases_last_run": {k: v[-1] for k, v in phases.items()}, "host": bench.host_info(threads),
-           "csv_byte_identical": same, "csv_bytes": len(first)}
+           "csv_byte_identical": same, "csv_bytes": len(first),
+           "csv_equals_reference_binary_digest": digest_ok}
     if "ref" in med:
         res["speedup_wall"] = round(med["ref"] / med["ours"], 1)
         if "dropin" in med:
             res["speedup_wall_dropin"] = round(med["ref"] / med["dropin"], 1)
     print(json.dumps(res), flush=True)
-    sys.exit(0 if same else 1)
+    sys.exit(0 if same and digest_ok is not False else 1)
 
 
 if __name__ == "__main__":

@@ -7,6 +7,10 @@
 #   stream     C5 shape: tools/gpu/stream_bench.py, 100 000 genomes, no-op sink
 #   stream_r05 the same against round 5's library
 #   bench      the bench line (bench.py --steps 20 --warmup 5, no CPU baseline)
+#   cyclic     one-GPU emulation of the 8-way split: contiguous vs block-cyclic (tools/gpu/shard_cyclic.py)
+#   stag       A/B of k_rows_pl's S5-entry variants (PFAAI_PL_STAG, diagnostics build)
+#   e2e        C2 end to end: ours and the drop-in (E2E_ARGS="" adds the reference, ~5 min)
+#   rehearse   bench.py's N > 1 flow with gloo on the one GPU (tools/gpu/rehearse_multi.sh)
 #   smoke      __graft_entry__.smoke()
 # Every step has its own time limit and the first failure ends the call.
 #   TAG=r06a STEPS="tests qt qt_r05" TESTS=tests/test_gpu_stream.py bash tools/gpu/r06.sh
@@ -26,6 +30,12 @@ for step in ${STEPS:-suite}; do
     stream) timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k.json" 2> "$OUT/stream.err" || exit 1 ;;
     stream_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k_r05.json" 2> "$OUT/stream_r05.err" || exit 1 ;;
     bench) timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline none > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1 ;;
+    cyclic) timeout -k 10 400 python3 -u tools/gpu/shard_cyclic.py 10000 8 --reps 5 > "$OUT/shard_cyclic.txt" 2> "$OUT/shard_cyclic.err" || exit 1 ;;
+    stag) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so timeout -k 10 400 python3 -u tools/gpu/ab_rows.py --genomes 10000 --rounds 7 \
+            --variants PFAAI_PL_STAG=0 PFAAI_PL_STAG=1 PFAAI_PL_STAG=2 PFAAI_PL_STAG=3 PFAAI_PL_STAG=4 PFAAI_PL_STAG=5 \
+            > "$OUT/ab_stag.txt" 2> "$OUT/ab_stag.err" || exit 1 ;;
+    e2e) timeout -k 10 900 python3 -u tools/gpu/e2e_c2.py --repeats 3 ${E2E_ARGS:---skip-ref} > "$OUT/e2e_c2.json" 2> "$OUT/e2e.err" || exit 1 ;;
+    rehearse) OUT="$OUT" bash tools/gpu/rehearse_multi.sh || exit 1 ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
