@@ -309,6 +309,12 @@ def main():
                          "rows' JAC segments go straight into rank 0's output by grouped send / recv).  The one-GPU "
                          "emulation (profiles/r06/shard_cyclic.txt) put the slowest cyclic rank at 1.08 ms against "
                          "1.05-1.09 contiguous, so the default stays contiguous")
+    ap.add_argument("--rccl-one-gpu", action="store_true",
+                    help="one-GPU box rehearsal of the N > 1 flow through RCCL itself (the nccl backend): every rank "
+                         "on device local %% device_count with its own NCCL_HOSTID, so RCCL takes the ranks for "
+                         "separate hosts (it refuses two ranks of one host on one device) and moves the data over "
+                         "its socket transport on the loopback interface instead of xGMI -- the RCCL send / recv / "
+                         "gather paths execute; not a measurement")
     ap.add_argument("--f-only", action="store_true",
                     help="give the engine F only (device radix-sort transposition instead of G)")
     ap.add_argument("--launch-dry-run", action="store_true",
@@ -333,8 +339,13 @@ def main():
     import torch.distributed as dist
 
     rehearse = args.rehearse_gloo and world > 1
-    if rehearse:  # (RCCL refuses two ranks on one device; gloo gathers host tensors)
+    one_gpu = args.rccl_one_gpu and world > 1 and not rehearse
+    if rehearse or one_gpu:  # (RCCL refuses two ranks of one host on one device; gloo gathers host tensors)
         local = local % max(1, torch.cuda.device_count())
+    if one_gpu:  # read by RCCL at its first communicator: one "host" per rank, loopback sockets
+        os.environ["NCCL_HOSTID"] = f"pfaai-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     hdev = torch.device("cpu") if rehearse else dev  # where the gathered blocks and reductions live
@@ -615,6 +626,9 @@ def main():
         }
         if rehearse:
             line["rehearsal"] = "gloo, all ranks on one GPU, gather through host memory: flow check, not a measurement"
+        if one_gpu:
+            line["rehearsal"] = ("RCCL (nccl backend), all ranks on one GPU as separate NCCL hosts, transfers over "
+                                 "RCCL's socket transport on loopback: the RCCL path executes; not a measurement")
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

@@ -88,18 +88,31 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         // the kernel offsets the window-major tables by its window index
         Dev dv = c->dev;
         dv.blk = static_cast<uint4*>(c->blkw.p);
-        // (V 4: S5 without the denominator clamp where T is every list's length)
-        constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2) : (kPlVG | 2);
-        const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 0: the QT quirk's per-column division
+        // (V 4: S5 without the denominator clamp where T is every list's
+        // length; V 32: 8-member tasks -- PFAAI_PL_NOT8=1 in the diagnostics
+        // build keeps 16-member ones, A/B)
+        constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2 | 32) : (kPlVG | 2 | 32);
+        const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 32 only: the QT quirk's per-column division
         const bool tx = c->t_exact;
         if (w_lo < nwin) {
             const int64_t r0 = rb, r1 = re;
             const int32_t ac = kWinGrid0 - w_lo;
             const int32_t gy = nwin - w_lo;
-            if (bigf) {
-                if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, VS | 4); else PLK(true, 4, VS);
-            } else {
-                if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, VS | 4); else PLK(false, 4, VS);
+#ifdef PFAAI_DIAGNOSTICS
+            if (DIAG_ENV("PFAAI_PL_NOT8")) {
+                if (bigf) {
+                    if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, (VS & ~32) | 4); else PLK(true, 4, VS & ~32);
+                } else {
+                    if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, (VS & ~32) | 4); else PLK(false, 4, VS & ~32);
+                }
+            } else
+#endif
+            {
+                if (bigf) {
+                    if (cm) PLK(true, 4, 32); else if (tx) PLK(true, 4, VS | 4); else PLK(true, 4, VS);
+                } else {
+                    if (cm) PLK(false, 4, 32); else if (tx) PLK(false, 4, VS | 4); else PLK(false, 4, VS);
+                }
             }
         }
         if constexpr (MODE == 0) {
@@ -218,6 +231,9 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
     case K: launch_k_rows<MODE, K>(c, rb, re, flags, aji, S, N, s); break;
     // N in LDS (P <= 255; PFAAI_PL_NREG=1 keeps it in registers, A/B)
     const bool nl = c->prob.n_prot <= 255 && !DIAG_ENV("PFAAI_PL_NREG");
+#ifdef PFAAI_DIAGNOSTICS
+    // (RK_PL512 is reachable only through PFAAI_ROWS_KERNEL: the release
+    // library compiles none of its instantiations)
     if constexpr (MODE != kModeFull) {  // full rows: k_rows_pl / fused only
         if (c->rows_kernel == RK_PL512) {
             // 512-thread workgroups, four per CU (<= 64 VGPRs), for A/B of
@@ -238,6 +254,7 @@ void launch_rows(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* a
             return;
         }
     }
+#endif
     if (c->rows_kernel == RK_PL || (MODE == kModeFull && c->rows_kernel != RK_FUSED)) {
         const char* km = DIAG_ENV("PFAAI_PL_KWMAX");  // diagnostics: cap the counter words per thread
         const int kw = pick_kw<1024>(c->cols_run, km ? std::max(1, std::min(5, atoi(km))) : 5);

@@ -124,12 +124,14 @@ __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, 
 // byte offset into F wraps -- buffer offsets, strided index included, are
 // 32-bit on gfx9): 64-bit global loads instead; a lane without members
 // re-reads F[0..7] (its mask bits are clear).
-template <int TC = kPlTaskCap, bool BIGF = false, bool A8 = false>
+// T8 (WK 4, V bit 32): tasks of 8 members, one per lane (gl8 = 0): task l of
+// a run starts at member 8 l of its 8-aligned span.
+template <int TC = kPlTaskCap, bool BIGF = false, bool A8 = false, bool T8 = false>
 __device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
                                                 const uint2* rt, int k, int nt, uint32_t gl8, uint4& b, uint4& bh) {
     const uint32_t t = tk[min(k, TC - 1)];
     const uint2 rr = rt[t & 1023u];
-    const uint32_t m0 = (rr.x & ~(uint32_t)(A8 ? 7 : kGroup - 1)) + ((t >> 6) & ~15u) + gl8;
+    const uint32_t m0 = (rr.x & ~(uint32_t)(A8 ? 7 : kGroup - 1)) + (T8 ? ((t >> 7) & ~7u) : ((t >> 6) & ~15u)) + gl8;
     const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 8);
     const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 8);
     uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
@@ -214,7 +216,8 @@ constexpr int kClkBlocks = 256;
 // per-column branches: the SALU of six exec-mask updates per word); 2 the
 // WK 3 member scatter by pl_scatter8_code over k_fcode's member codes; 8
 // S5's two divisions of a word by one reciprocal (exact_div_pair, with 1);
-// 16 the G entries one protein ahead instead of two (WK 3, ONE below); 4
+// 16 the G entries one protein ahead instead of two (WK 3, ONE below); 32
+// 8-member tasks, one per lane (WK 4, T8 below); 4
 // S5 without the max(d, 1) clamp outside WK 3 too (launched only on loads
 // whose T is every list's length, t_exact -- WK 3 implies it); 64
 // the reference-compat quirks compiled out (MODE 2 launches it only without
@@ -245,7 +248,14 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr bool NL = NK == 1;
     constexpr int NN = NK == 0 ? KW : 1;  // N registers
     constexpr int TC = NL ? kPlTaskCap / 2 : kPlTaskCap;  // line tasks per stage (half where LDS holds N)
-    constexpr int NGX = NT / 2;                           // lane pairs (one line task each per round)
+    // T8 (V bit 32, WK 4 only): 8-member tasks, one per lane, instead of
+    // 16-member tasks per lane pair.  A window sub-run holds ~20 members at
+    // C4 / C5 sizes, so 16-member tasks from an 8-aligned start fill ~60 %
+    // of their slots and a protein needed two rounds of member loads (~580
+    // tasks for 512 lane pairs), the second one's load latency exposed; in
+    // 8-member tasks the same members fit one round of 1024 lanes
+    constexpr bool T8 = (V & 32) != 0 && WK == 4;
+    constexpr int NGX = T8 ? NT : NT / 2;                 // task takers per round (lane pairs; T8: lanes)
     extern __shared__ uint32_t pl_smem[];                 // acc[2][W], goff[P + 1], (NL) n32, taL
     __shared__ uint2 rt[2][kPlEntries];                   // runs of a protein stage: member range [lo, hi)
     __shared__ uint16_t tk[2][TC];                        // line tasks
@@ -393,9 +403,9 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
             } else if constexpr (WK == 4) {
                 // the window sub-run is exactly A's partners in the window:
-                // 16-member tasks from an 8-aligned start, as WK 3
+                // 16-member tasks from an 8-aligned start, as WK 3 (T8: 8-member tasks)
                 r = make_uint2(r4[j].x, r4[j].y);  // OOB entries: (0, 0), empty
-                nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
+                nl[j] = r.y > r.x ? (T8 ? (r.y - (r.x & ~7u) + 7u) >> 3 : (r.y - (r.x & ~7u) + 15u) >> 4) : 0u;
             } else {
                 nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && win >= 0));
             }
@@ -536,12 +546,12 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     uint32_t twc[KW];  // T words of the previous protein, carried across the barrier
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
-    const uint32_t gl8 = 8u * (uint32_t)(tid & 1);
+    const uint32_t gl8 = T8 ? 0u : 8u * (uint32_t)(tid & 1);
     const uint32_t wspan = (uint32_t)(whi - wlo);
-    const int grpx = tid >> 1;
+    const int grpx = T8 ? tid : tid >> 1;
     int st_cur = 0;
     auto issue2 = [&](int k, int ntk, uint4& bb, uint4& bbh) -> uint32_t {
-        return pl_issue_m2<TC, BIGF, GP || WK == 4>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
+        return pl_issue_m2<TC, BIGF, GP || WK == 4, T8>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
     };
     auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
         if constexpr (CODE) {

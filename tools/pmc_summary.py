@@ -14,7 +14,9 @@ calibrated only for 16-B-per-lane streaming reads.  k_rows' reads are 4-8 B
 gathers (member ids, work records, T entries), so the raw figure is used and
 the x2 figure is recorded next to it as an upper bound.
 
-usage: python tools/pmc_summary.py gpurun_out/pmc r01
+usage: python tools/pmc_summary.py gpurun_out/pmc r01 [--no-k-rows] [--what "..."]
+  --no-k-rows   a profile of another workload (C4, C5): write only
+                profiles/<tag>_pmc.json, not bench.py's pmc_k_rows.json
 """
 import collections
 import csv
@@ -70,8 +72,12 @@ def derive(c):
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-    tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    d = args[0] if args else "gpurun_out/pmc"
+    tag = args[1] if len(args) > 1 else "r01"
+    what = sys.argv[sys.argv.index("--what") + 1] if "--what" in sys.argv else "10k SYN all-vs-all"
+    if "--what" in sys.argv:
+        args.remove(what) if what in args else None
     ks = collect(d)
     if not ks:
         sys.exit(f"no counter CSVs under {d}")
@@ -79,7 +85,7 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
-        json.dump({"source": "rocprofv3 --pmc --kernel-trace, tools/gpu/pmc.sh, 10k SYN all-vs-all",
+        json.dump({"source": f"rocprofv3 --pmc --kernel-trace, one counter group per pass, {what}",
                    "kernels": res}, f, indent=1, sort_keys=True)
     # One all-vs-all step may run two row kernels at once (pfaai_launch.hpp
     # launch_narrow: the wide rows as 1024-thread workgroups on the step's
@@ -88,7 +94,7 @@ def main():
     # of their cycles, since counter collection serialises the dispatches.
     rows = sorted((k for k in res if "k_rows" in k),
                   key=lambda k: -res[k]["derived"].get("kernel_cycles", 0))
-    if rows:
+    if rows and "--no-k-rows" not in sys.argv:
         k = rows[0]
         dv = res[k]["derived"]
 
