@@ -21,6 +21,7 @@ carries the binaries.
 from __future__ import annotations
 
 import os
+import time
 import subprocess
 import sys
 
@@ -50,8 +51,6 @@ def build_hip(force=False, diag=False):
     units = sorted(f for f in os.listdir(csrc) if f.endswith(".hip"))
     deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include/pfaai_hip.h")]
     out = os.path.join(ROOT, "parfastaai_amd/lib", "libpfaai_hip_diag.so" if diag else "libpfaai_hip.so")
-    if not (force or _newer(out, deps)):
-        return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     objdir = os.path.join(ROOT, "build", "hip_diag" if diag else "hip")
     os.makedirs(objdir, exist_ok=True)
@@ -64,9 +63,22 @@ def build_hip(force=False, diag=False):
     # (a row-kernel unit takes ~4 min: editing the C-ABI unit alone must not
     # recompile them)
     headers = [d for d in deps if not d.endswith(".hip")]
+    # (by object, not by the library: a header edited while an earlier build
+    # compiled would otherwise be older than that build's library and never
+    # reach the objects compiled before the edit)
     todo = [(u, o) for u, o in zip(units, objs) if force or _newer(o, [os.path.join(csrc, u), *headers])]
+    if not todo and not _newer(out, objs):
+        return out
+    def compile_unit(u, o):
+        # the object carries the time its compile STARTED: a header edited
+        # while the compile ran is then newer than the object, and the next
+        # build compiles the unit again instead of keeping a mixed library
+        t0 = time.time()
+        _run([HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)])
+        os.utime(o, (t0, t0))
+
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), int(os.environ.get("MAX_JOBS", "8"))))) as ex:
-        futs = [ex.submit(_run, [HIPCC, *flags, "-c", "-o", o, os.path.join(csrc, u)]) for u, o in todo]
+        futs = [ex.submit(compile_unit, u, o) for u, o in todo]
         for f in futs:
             f.result()  # re-raises a failed compile
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs, "-ldl"])
