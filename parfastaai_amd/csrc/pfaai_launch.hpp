@@ -89,29 +89,40 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         Dev dv = c->dev;
         dv.blk = static_cast<uint4*>(c->blkw.p);
         // (V 4: S5 without the denominator clamp where T is every list's
-        // length; V 32: 8-member tasks -- PFAAI_PL_NOT8=1 in the diagnostics
-        // build keeps 16-member ones, A/B)
-        constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2 | 32) : (kPlVG | 2 | 32);
-        const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 32 only: the QT quirk's per-column division
+        // length.  V 32, 8-member tasks, only in the diagnostics build behind
+        // PFAAI_PL_T8=1: measured slower, C4 rows 6.92 -> 11.05 ms, C5 rows
+        // 545 -> 643 ms, profiles/r06/qt_c4_t8_ab.txt)
+        constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2) : (kPlVG | 2);
+        const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 0: the QT quirk's per-column division
         const bool tx = c->t_exact;
         if (w_lo < nwin) {
             const int64_t r0 = rb, r1 = re;
             const int32_t ac = kWinGrid0 - w_lo;
             const int32_t gy = nwin - w_lo;
 #ifdef PFAAI_DIAGNOSTICS
-            if (DIAG_ENV("PFAAI_PL_NOT8")) {
+            // stage clocks of the query-vs-target window spans (PFAAI_PL_CLK,
+            // tools/gpu/stage_clocks.py --qt): the release form with the clock registers
+            if constexpr (MODE == 2 && KW == 5 && NT == 1024) {
+                if (!bigf && !cm && tx && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+                    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, 4, VS | 4>), dim3(r1 - r0, gy),
+                                       dim3(NT), lds, s, dv, r0, chunk, ac, flags, sc + SC_FIRST_KEY, aji, S, N,
+                                       sc + SC_EVENTS, static_cast<unsigned long long*>(c->dbg.p));
+                    return;
+                }
+            }
+            if (DIAG_ENV("PFAAI_PL_T8")) {
                 if (bigf) {
-                    if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, (VS & ~32) | 4); else PLK(true, 4, VS & ~32);
+                    if (cm) PLK(true, 4, 32); else if (tx) PLK(true, 4, VS | 32 | 4); else PLK(true, 4, VS | 32);
                 } else {
-                    if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, (VS & ~32) | 4); else PLK(false, 4, VS & ~32);
+                    if (cm) PLK(false, 4, 32); else if (tx) PLK(false, 4, VS | 32 | 4); else PLK(false, 4, VS | 32);
                 }
             } else
 #endif
             {
                 if (bigf) {
-                    if (cm) PLK(true, 4, 32); else if (tx) PLK(true, 4, VS | 4); else PLK(true, 4, VS);
+                    if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, VS | 4); else PLK(true, 4, VS);
                 } else {
-                    if (cm) PLK(false, 4, 32); else if (tx) PLK(false, 4, VS | 4); else PLK(false, 4, VS);
+                    if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, VS | 4); else PLK(false, 4, VS);
                 }
             }
         }

@@ -2,7 +2,7 @@
 --diag`, loaded through PFAAI_HIP_LIB): where the protein loop's time goes,
 per stage, for the waves of the first 256 workgroups of the launch.
 
-    python tools/gpu/stage_clocks.py [--genomes 10000] [--v2] [--rows lo:hi]
+    python tools/gpu/stage_clocks.py [--genomes 10000] [--v2] [--rows lo:hi] [--qt 50000:1000]
 k_rows_pl (PFAAI_PL_CLK) by default, k_rows_v2 (PFAAI_V2_CLK) with --v2.
 """
 import argparse
@@ -24,11 +24,27 @@ ap.add_argument("--genomes", type=int, default=10000)
 ap.add_argument("--v2", action="store_true")
 ap.add_argument("--rows", default=None, help="row range lo:hi (default: all rows)")
 ap.add_argument("--la", action="store_true", help="stage names of k_rows_pl's lookahead form (narrow launches)")
+ap.add_argument("--qt", default=None, help="targets:queries -- the query-vs-target (C4) shape of tools/gpu/qt_bench.py "
+                "(window spans) instead of all-vs-all")
 a = ap.parse_args()
-g = syn.generate(a.genomes, 100)
-ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
 eng = _capi.Engine(0)
-eng.load(**ds.problem())
+if a.qt:
+    nT, nQ = (int(x) for x in a.qt.split(":"))
+    K = 20
+    gt = syn.generate(nT, 100, clade_size=K)
+    gq = syn.generate(nQ, 100, clade_size=K, genome_seed=syn.DEFAULT_SEED + 1, n_clades=(nT + K - 1) // K,
+                      clade_mod=True)
+    m = syn.qt_merge(gt, gq)
+    del gt, gq
+    is_q = np.zeros(nT + nQ, np.uint8)
+    is_q[nT:] = 1
+    eng.load(mode=_capi.MODE_QT, n_ids=nT + nQ, n_prot=100, n_qry=nQ, n_tgt=nT, is_q=is_q, Lp=m["Lp"],
+             F_prot=m["F_prot"], F_genome=m["F_genome"], T=m["T"], G_off=m["G_off"], G_tet=m["G_tet"])
+    del m
+else:
+    g = syn.generate(a.genomes, 100)
+    ds = ParFAAIData.from_split(g["Lp"], g["F_prot"], g["F_genome"], g["T"]).with_genome_major(g["G_off"], g["G_tet"])
+    eng.load(**ds.problem())
 rows, pairs = eng.shape()
 r0, r1 = (int(x) for x in a.rows.split(":")) if a.rows else (0, rows)
 d = eng.alloc(pairs * 8)
