@@ -89,9 +89,11 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
         Dev dv = c->dev;
         dv.blk = static_cast<uint4*>(c->blkw.p);
         // (V 4: S5 without the denominator clamp where T is every list's
-        // length.  V 32, 8-member tasks, only in the diagnostics build behind
-        // PFAAI_PL_T8=1: measured slower, C4 rows 6.92 -> 11.05 ms, C5 rows
-        // 545 -> 643 ms, profiles/r06/qt_c4_t8_ab.txt)
+        // length.  V 32, 24-member tasks, only in the diagnostics build behind
+        // PFAAI_PL_T24=1: fewer member rounds but slower, C4 rows 6.62 -> 6.87
+        // ms, C5 rows 531 -> 557 ms (profiles/r06/ab_t24.txt); 8-member tasks,
+        // one per lane, were slower still: C4 rows 6.92 -> 11.05 ms, C5 545 ->
+        // 643 ms, profiles/r06/qt_c4_t8_ab.txt)
         constexpr int VS = MODE == 2 ? (kPlVG | 64 | 2) : (kPlVG | 2);
         const bool cm = MODE == 2 && (flags & PFAAI_FLAG_REF_COMPAT);  // V 0: the QT quirk's per-column division
         const bool tx = c->t_exact;
@@ -103,18 +105,36 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
             // stage clocks of the query-vs-target window spans (PFAAI_PL_CLK,
             // tools/gpu/stage_clocks.py --qt): the release form with the clock registers
             if constexpr (MODE == 2 && KW == 5 && NT == 1024) {
-                if (!bigf && !cm && tx && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
-                    hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, 4, VS | 4>), dim3(r1 - r0, gy),
-                                       dim3(NT), lds, s, dv, r0, chunk, ac, flags, sc + SC_FIRST_KEY, aji, S, N,
-                                       sc + SC_EVENTS, static_cast<unsigned long long*>(c->dbg.p));
+                if (!cm && tx && DIAG_ENV("PFAAI_PL_CLK") && c->dbg.bytes >= kClkBlocks * 16 * 8 * 8) {
+                    auto* clk = static_cast<unsigned long long*>(c->dbg.p);
+                    const bool t24 = DIAG_ENV("PFAAI_PL_T24") != nullptr;
+                    if (bigf) {
+                        if (t24)
+                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, true, 4, VS | 32 | 4>),
+                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, ac, flags,
+                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
+                        else
+                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, true, 4, VS | 4>),
+                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, ac, flags,
+                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
+                    } else {
+                        if (t24)
+                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, 4, VS | 32 | 4>),
+                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, ac, flags,
+                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
+                        else
+                            hipLaunchKernelGGL((k_rows_pl<MODE, KW, NT, WPE, true, NK, false, 4, VS | 4>),
+                                               dim3(r1 - r0, gy), dim3(NT), lds, s, dv, r0, chunk, ac, flags,
+                                               sc + SC_FIRST_KEY, aji, S, N, sc + SC_EVENTS, clk);
+                    }
                     return;
                 }
             }
-            if (DIAG_ENV("PFAAI_PL_T8")) {
+            if (DIAG_ENV("PFAAI_PL_T24")) {
                 if (bigf) {
-                    if (cm) PLK(true, 4, 32); else if (tx) PLK(true, 4, VS | 32 | 4); else PLK(true, 4, VS | 32);
+                    if (cm) PLK(true, 4, 0); else if (tx) PLK(true, 4, VS | 32 | 4); else PLK(true, 4, VS | 32);
                 } else {
-                    if (cm) PLK(false, 4, 32); else if (tx) PLK(false, 4, VS | 32 | 4); else PLK(false, 4, VS | 32);
+                    if (cm) PLK(false, 4, 0); else if (tx) PLK(false, 4, VS | 32 | 4); else PLK(false, 4, VS | 32);
                 }
             } else
 #endif
@@ -130,7 +150,11 @@ void launch_pl(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji
             const int64_t r0 = rb, r1 = re;
             const int32_t ac = kWinDiag;
             const int32_t gy = 1;
-            if (bigf) PLK(true, 1, kPlVG); else PLK(false, 1, kPlVG);
+            if (tx) {  // (V 4 as above)
+                if (bigf) PLK(true, 1, kPlVG | 4); else PLK(false, 1, kPlVG | 4);
+            } else {
+                if (bigf) PLK(true, 1, kPlVG); else PLK(false, 1, kPlVG);
+            }
         }
         return;
     }

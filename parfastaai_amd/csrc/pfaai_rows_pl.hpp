@@ -124,14 +124,12 @@ __device__ __forceinline__ void pl_scatter4_m(const Dev& d, int32_t a, uint4 b, 
 // byte offset into F wraps -- buffer offsets, strided index included, are
 // 32-bit on gfx9): 64-bit global loads instead; a lane without members
 // re-reads F[0..7] (its mask bits are clear).
-// T8 (WK 4, V bit 32): tasks of 8 members, one per lane (gl8 = 0): task l of
-// a run starts at member 8 l of its 8-aligned span.
-template <int TC = kPlTaskCap, bool BIGF = false, bool A8 = false, bool T8 = false>
+template <int TC = kPlTaskCap, bool BIGF = false, bool A8 = false>
 __device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
                                                 const uint2* rt, int k, int nt, uint32_t gl8, uint4& b, uint4& bh) {
     const uint32_t t = tk[min(k, TC - 1)];
     const uint2 rr = rt[t & 1023u];
-    const uint32_t m0 = (rr.x & ~(uint32_t)(A8 ? 7 : kGroup - 1)) + (T8 ? ((t >> 7) & ~7u) : ((t >> 6) & ~15u)) + gl8;
+    const uint32_t m0 = (rr.x & ~(uint32_t)(A8 ? 7 : kGroup - 1)) + ((t >> 6) & ~15u) + gl8;
     const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 8);
     const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 8);
     uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
@@ -142,6 +140,36 @@ __device__ __forceinline__ uint32_t pl_issue_m2(rsrc_t fg, const int32_t* __rest
     } else {
         b = bld_u128(fg, (mask & 15u) ? m0 * 4u : kOOB, 0u);
         bh = bld_u128(fg, (mask >> 4) ? m0 * 4u + 16u : kOOB, 0u);
+    }
+    return mask;
+}
+
+// T24 (WK 4, V bit 32): 24-member tasks from an 8-aligned start, 12 members
+// per lane of the pair (gl12 = 12 * (tid & 1)) by three 16-B loads: task l of
+// a run starts at member 24 l of its 8-aligned span; the mask has 12 bits.
+template <int TC = kPlTaskCap, bool BIGF = false>
+__device__ __forceinline__ uint32_t pl_issue_m3(rsrc_t fg, const int32_t* __restrict__ Fg, const uint16_t* tk,
+                                                const uint2* rt, int k, int nt, uint32_t gl12, uint4& b, uint4& bh,
+                                                uint4& bx) {
+    const uint32_t t = tk[min(k, TC - 1)];
+    const uint2 rr = rt[t & 1023u];
+    const uint32_t m0 = (rr.x & ~7u) + (t >> 10) * 24u + gl12;
+    const int32_t l0 = min(max((int32_t)(rr.x - m0), 0), 12);
+    const int32_t h0 = min(max((int32_t)(rr.y - m0), l0), 12);
+    uint32_t mask = ((1u << (uint32_t)(h0 - l0)) - 1u) << (uint32_t)l0;
+    if (!(k < nt && t != kPlNoTask)) mask = 0u;
+    if constexpr (BIGF) {
+        // one 64-bit address for the three pieces (F[0..11] where the lane has
+        // no task; a piece without members re-reads its task's lines, which
+        // F's 16 padding entries keep in range)
+        const uint4* pb = reinterpret_cast<const uint4*>(Fg + (mask ? m0 : 0u));
+        b = pb[0];
+        bh = pb[1];
+        bx = pb[2];
+    } else {
+        b = bld_u128(fg, (mask & 15u) ? m0 * 4u : kOOB, 0u);
+        bh = bld_u128(fg, (mask & 0xF0u) ? m0 * 4u + 16u : kOOB, 0u);
+        bx = bld_u128(fg, (mask >> 8) ? m0 * 4u + 32u : kOOB, 0u);
     }
     return mask;
 }
@@ -194,6 +222,25 @@ __device__ __forceinline__ void pl_scatter8_code(uint4 c, uint4 ch, uint32_t m, 
 #undef PL_SLOT
 }
 
+// pl_scatter8_code's slots for a third 16-B piece (T24: members 8-11 of the lane)
+__device__ __forceinline__ void pl_scatter4_code(uint4 c, uint32_t m, uint32_t base) {
+    uint64_t sv;
+    uint32_t t, u;
+#define PL_SLOT(BIT, R)                              \
+    "v_and_b32 %[t], " #BIT ", %[m]\n\t"              \
+    "v_cmpx_ne_u32_e32 vcc, 0, %[t]\n\t"              \
+    "v_lshrrev_b32 %[t], 5, %[" R "]\n\t"             \
+    "v_add_u32 %[t], %[base], %[t]\n\t"               \
+    "v_lshlrev_b32_e64 %[u], %[" R "], 1\n\t"         \
+    "ds_add_u32 %[t], %[u]\n\t"                       \
+    "s_mov_b64 exec, %[sv]\n\t"
+    asm volatile("s_mov_b64 %[sv], exec\n\t" PL_SLOT(1, "c0") PL_SLOT(2, "c1") PL_SLOT(4, "c2") PL_SLOT(8, "c3")
+                 : [sv] "=&s"(sv), [t] "=&v"(t), [u] "=&v"(u)
+                 : [m] "v"(m), [base] "s"(base), [c0] "v"(c.x), [c1] "v"(c.y), [c2] "v"(c.z), [c3] "v"(c.w)
+                 : "vcc", "memory");
+#undef PL_SLOT
+}
+
 // CLK (diagnostics, PFAAI_PL_CLK): every wave of the first kClkBlocks
 // workgroups sums the shader-clock time of each stage of the protein loop
 // into clk[(block * (NT / 64) + wave) * 8 + stage] (pfaai_debug_clocks,
@@ -217,7 +264,7 @@ constexpr int kClkBlocks = 256;
 // WK 3 member scatter by pl_scatter8_code over k_fcode's member codes; 8
 // S5's two divisions of a word by one reciprocal (exact_div_pair, with 1);
 // 16 the G entries one protein ahead instead of two (WK 3, ONE below); 32
-// 8-member tasks, one per lane (WK 4, T8 below); 4
+// 24-member tasks, 12 members per lane (WK 4, T24 below); 4
 // S5 without the max(d, 1) clamp outside WK 3 too (launched only on loads
 // whose T is every list's length, t_exact -- WK 3 implies it); 64
 // the reference-compat quirks compiled out (MODE 2 launches it only without
@@ -248,14 +295,20 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     constexpr bool NL = NK == 1;
     constexpr int NN = NK == 0 ? KW : 1;  // N registers
     constexpr int TC = NL ? kPlTaskCap / 2 : kPlTaskCap;  // line tasks per stage (half where LDS holds N)
-    // T8 (V bit 32, WK 4 only): 8-member tasks, one per lane, instead of
-    // 16-member tasks per lane pair.  A window sub-run holds ~20 members at
-    // C4 / C5 sizes, so 16-member tasks from an 8-aligned start fill ~60 %
-    // of their slots and a protein needed two rounds of member loads (~580
-    // tasks for 512 lane pairs), the second one's load latency exposed; in
-    // 8-member tasks the same members fit one round of 1024 lanes
-    constexpr bool T8 = (V & 32) != 0 && WK == 4;
-    constexpr int NGX = T8 ? NT : NT / 2;                 // task takers per round (lane pairs; T8: lanes)
+    // T24 (V bit 32, WK 4 with the member codes): 24-member tasks per lane
+    // pair (12 members a lane, three 16-B loads) instead of 16.  A protein's
+    // window sub-runs at C4 / C5 sizes are mostly one clade's clump of ~18
+    // members: 16-member tasks from an 8-aligned start take two tasks for it,
+    // and a protein's tasks needed 1.64 rounds of 512 lane pairs on average
+    // (C4 shape, 25k targets: the rounds after the first, each with its load
+    // latency exposed, were a third of the loop, profiles/r06/
+    // stage_clocks_qt25k.txt); 24-member tasks need 1.29 -- yet measured
+    // slower (C4 rows 6.62 -> 6.87 ms, C5 531 -> 557 ms: a third load and four
+    // scatter slots per lane on every round, one spilled VGPR), so a
+    // diagnostics variant only.  (8-member tasks, one per lane, overflowed the
+    // task list: C4 rows 6.92 -> 11.05 ms.)
+    constexpr bool T24 = (V & 32) != 0 && WK == 4 && (V & 2) != 0;
+    constexpr int NGX = NT / 2;                           // task takers per round (lane pairs)
     extern __shared__ uint32_t pl_smem[];                 // acc[2][W], goff[P + 1], (NL) n32, taL
     __shared__ uint2 rt[2][kPlEntries];                   // runs of a protein stage: member range [lo, hi)
     __shared__ uint16_t tk[2][TC];                        // line tasks
@@ -314,7 +367,6 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     for (int k = 0; k < KW; ++k) { S[2 * k] = 0.0; S[2 * k + 1] = 0.0; }
 #pragma unroll
     for (int k = 0; k < NN; ++k) N[k] = 0u;
-    uint32_t ev = 0;
     __syncthreads();
 
     // Fg carries 16 padding entries and the range covers them: a 16-B load
@@ -379,6 +431,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 (void)e;
                 gq2[j] = gq[j];
                 r4[j].y = (uint32_t)gt[j];  // G_end (S1)
+            } else if constexpr (WK == 4) {  // the window sub-run (lo, hi) only
+                const uint2 v = bld_u64(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB,
+                                        (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
+                r4[j] = make_uint4(v.x, v.y, 0u, 0u);
             } else {
                 r4[j] = bld_u128(r_blk, e < n ? (uint32_t)gt[j] * 16u : kOOB,
                                  (uint32_t)min(p, P - 1) * (kNTetramers * 16u));
@@ -390,6 +446,11 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     // register copy under WK 3, and its second stage holds 2 VGPRs across the
     // whole iteration
     constexpr bool ONE = GP && (V & 16) != 0;
+    // |E| (the sum of the counters) under WK 3 / 4 is the sum of the walked
+    // run lengths -- every member of [r.x, r.y) is one event in the window --
+    // so S3 counts it per entry instead of S5 per counter word
+    constexpr bool EV3 = WK == 3 || WK == 4;
+    uint32_t ev = 0;
     auto s3 = [&](int q, const uint4 (&r4)[EPT], const uint32_t (&gq2)[EPT], const int32_t (&gt1)[EPT]) {  // line tasks of protein q
         const int st = q & 1, cs = q % 3;
         if (wbase0 >= glen(q)) return;
@@ -403,13 +464,18 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 nl[j] = r.y > r.x ? (r.y - (r.x & ~7u) + 15u) >> 4 : 0u;
             } else if constexpr (WK == 4) {
                 // the window sub-run is exactly A's partners in the window:
-                // 16-member tasks from an 8-aligned start, as WK 3 (T8: 8-member tasks)
+                // 16-member tasks from an 8-aligned start, as WK 3 (T24: 24-member
+                // tasks; x / 24 = x * 43691 >> 20 exactly below 2^16, and any
+                // span past that is a whole-workgroup run either way)
                 r = make_uint2(r4[j].x, r4[j].y);  // OOB entries: (0, 0), empty
-                nl[j] = r.y > r.x ? (T8 ? (r.y - (r.x & ~7u) + 7u) >> 3 : (r.y - (r.x & ~7u) + 15u) >> 4) : 0u;
+                nl[j] = r.y > r.x ? (T24 ? (min(r.y - (r.x & ~7u) + 23u, 65535u) * 43691u) >> 20
+                                         : (r.y - (r.x & ~7u) + 15u) >> 4)
+                                  : 0u;
             } else {
                 nl[j] = run_lines(r4[j], wlo, whi, r, min_len, !(MODE == 2 && win >= 0));
             }
             rt[st][e] = r;
+            if constexpr (EV3) ev += r.y > r.x ? r.y - r.x : 0u;
             if (nl[j] > (uint32_t)kPlMaxLines) {
                 atomicOr(&wmask[cs][e >> 5], 1u << (e & 31));
                 atomicAdd(&nwhole[cs], 1u);
@@ -508,7 +574,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                 if (v) {
                     acc_p[w] = 0u;
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                    ev += (uint32_t)(c0 + c1);
+                    if constexpr (!EV3) ev += (uint32_t)(c0 + c1);
                     n_add(k, v);
                     int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
                     if constexpr (WK != 3 && (V & 4) == 0) {
@@ -535,7 +601,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             if (v) {
                 acc_p[w] = 0u;
                 const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
-                ev += (uint32_t)(c0 + c1);
+                if constexpr (!EV3) ev += (uint32_t)(c0 + c1);
                 n_add(k, v);
                 const int32_t d0 = ta + (int32_t)(tw[k] & 0xFFFFu) - c0, d1 = ta + (int32_t)(tw[k] >> 16) - c1;
                 if (c0) S[2 * k] += div(c0, d0);
@@ -546,17 +612,22 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     uint32_t twc[KW];  // T words of the previous protein, carried across the barrier
 #pragma unroll
     for (int k = 0; k < KW; ++k) twc[k] = 0u;
-    const uint32_t gl8 = T8 ? 0u : 8u * (uint32_t)(tid & 1);
+    const uint32_t gl8 = (T24 ? 12u : 8u) * (uint32_t)(tid & 1);
     const uint32_t wspan = (uint32_t)(whi - wlo);
-    const int grpx = T8 ? tid : tid >> 1;
+    const int grpx = tid >> 1;
     int st_cur = 0;
+    uint4 bx = make_uint4(0u, 0u, 0u, 0u);  // T24: the lane's members 8-11
     auto issue2 = [&](int k, int ntk, uint4& bb, uint4& bbh) -> uint32_t {
-        return pl_issue_m2<TC, BIGF, GP || WK == 4, T8>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
+        if constexpr (T24)
+            return pl_issue_m3<TC, BIGF>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh, bx);
+        else
+            return pl_issue_m2<TC, BIGF, GP || WK == 4>(r_fm, Fm, tk[st_cur], rt[st_cur], k, ntk, gl8, bb, bbh);
     };
     auto scatter8 = [&](uint32_t* acc_x, uint4 bb, uint4 bbh, uint32_t m) {
         if constexpr (CODE) {
             const uint32_t base = uni_u32((uint32_t)(uintptr_t)acc_x - 2u * (uint32_t)cc0);
             pl_scatter8_code(bb, bbh, m, base);
+            if constexpr (T24) pl_scatter4_code(bx, m >> 8, base);
         } else {
             pl_scatter4_m<MODE, WK>(d, a, bb, m & 15u, acc_x - (cc0 >> 1), wlo, wspan);
             pl_scatter4_m<MODE, WK>(d, a, bbh, m >> 4, acc_x - (cc0 >> 1), wlo, wspan);
@@ -645,8 +716,19 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
                         const int s = __builtin_ctz(m);
                         m &= m - 1u;
                         const uint32_t rx = uni_u32(rt[st][wd * 32 + s].x), ry = uni_u32(rt[st][wd * 32 + s].y);
-                        for (uint32_t mm = rx + tid; mm < ry; mm += NT)
-                            pl_add<MODE>(d, a, d.Fg[mm], acc_i, cc0, wlo, whi);
+                        // four loads in flight per lane (a run of 10 240 members
+                        // otherwise took ten dependent HBM round trips)
+                        uint32_t mm = rx + tid;
+                        const uint32_t lim = ry > 3u * NT ? ry - 3u * NT : 0u;
+                        for (; mm < lim; mm += 4u * NT) {
+                            const int32_t b0 = d.Fg[mm], b1 = d.Fg[mm + NT], b2 = d.Fg[mm + 2u * NT],
+                                          b3 = d.Fg[mm + 3u * NT];
+                            pl_add<MODE>(d, a, b0, acc_i, cc0, wlo, whi);
+                            pl_add<MODE>(d, a, b1, acc_i, cc0, wlo, whi);
+                            pl_add<MODE>(d, a, b2, acc_i, cc0, wlo, whi);
+                            pl_add<MODE>(d, a, b3, acc_i, cc0, wlo, whi);
+                        }
+                        for (; mm < ry; mm += NT) pl_add<MODE>(d, a, d.Fg[mm], acc_i, cc0, wlo, whi);
                     }
                 }
             }

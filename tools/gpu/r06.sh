@@ -4,8 +4,9 @@
 #   tests      the tests named in TESTS (pytest node ids / files)
 #   qt         C4 shape: tools/gpu/qt_bench.py (50 000 targets x 1 000 queries)
 #   qt_r05     the same against round 5's library (tools/_build/ab, A/B)
-#   qt_t8 / qt_diag  the C4 run in the diagnostics build with / without PFAAI_PL_T8 (A/B of 8-member tasks)
+#   qt_t24 / qt_diag  the C4 run in the diagnostics build with / without PFAAI_PL_T24 (A/B of 24-member tasks)
 #   stream     C5 shape: tools/gpu/stream_bench.py, 100 000 genomes, no-op sink
+#   stream_t24 / stream_diag  the C5 run in the diagnostics build with / without PFAAI_PL_T24 (no re-check)
 #   stream_r05 the same against round 5's library
 #   bench      the bench line (bench.py --steps 20 --warmup 5, no CPU baseline)
 #   cyclic     one-GPU emulation of the 8-way split: contiguous vs block-cyclic (tools/gpu/shard_cyclic.py)
@@ -28,9 +29,11 @@ for step in ${STEPS:-suite}; do
     tests) timeout -k 10 900 $PYT $TESTS > "$OUT/tests_sel.txt" 2>&1 || { tail -30 "$OUT/tests_sel.txt"; exit 1; } ;;
     qt) timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4.json" 2> "$OUT/qt.err" || exit 1 ;;
     qt_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4_r05.json" 2> "$OUT/qt_r05.err" || exit 1 ;;
-    qt_t8) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so PFAAI_PL_T8=1 timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4_t8_diag.json" 2> "$OUT/qt_t8.err" || exit 1 ;;
+    qt_t24) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so PFAAI_PL_T24=1 timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4_t24_diag.json" 2> "$OUT/qt_t24.err" || exit 1 ;;
     qt_diag) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so timeout -k 10 500 python3 -u tools/gpu/qt_bench.py > "$OUT/qt_c4_diag.json" 2> "$OUT/qt_diag.err" || exit 1 ;;
     stream) timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k.json" 2> "$OUT/stream.err" || exit 1 ;;
+    stream_t24) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so PFAAI_PL_T24=1 timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop --check-rows 0 > "$OUT/stream_100k_t24_diag.json" 2> "$OUT/stream_t24.err" || exit 1 ;;
+    stream_diag) PFAAI_HIP_LIB=parfastaai_amd/lib/libpfaai_hip_diag.so timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop --check-rows 0 > "$OUT/stream_100k_diag.json" 2> "$OUT/stream_diag.err" || exit 1 ;;
     stream_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k_r05.json" 2> "$OUT/stream_r05.err" || exit 1 ;;
     bench) timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline none > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1 ;;
     cyclic) timeout -k 10 400 python3 -u tools/gpu/shard_cyclic.py 10000 8 --reps 5 > "$OUT/shard_cyclic.txt" 2> "$OUT/shard_cyclic.err" || exit 1 ;;
