@@ -1011,7 +1011,10 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
 #pragma unroll
         for (int q = 0; q < BPT; ++q) {
             const int b = tid * BPT + q;
-            if (b < BINS) lstart[b] = off;
+            if (b < BINS) {
+                lstart[b] = off;
+                gbase[b] -= off;  // the write phase's pos = gbase[d] + lp: one LDS read a record, not two
+            }
             off += tot[q];
         }
         if (tid == NT - 1) s_tn = off;  // (the tile's records, all digits)
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             for (int k = 0; k < kWH; ++k) {
                 const int lp = min(tid + (h + k) * NT, max(tn - 1, 0));
                 const uint32_t d = sort_digit(val[k], shift, mask);
-                pos[k] = gbase[d] + (uint32_t)(lp - (int)lstart[d]);
+                pos[k] = gbase[d] + (uint32_t)lp;  // (gbase[d] >= lstart[d]: the tile's records before digit d precede it)
             }
 #pragma unroll
             for (int k = 0; k < kWH; ++k) aux[k] = dst.fetch(pos[k], val[k]);
