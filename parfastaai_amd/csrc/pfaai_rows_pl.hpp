@@ -343,6 +343,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const bool compat = (V & 64) != 0 ? false : (flags & 1u) != 0;  // V 64: launched only without REF_COMPAT
     const uint32_t min_len = win >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
     const uint32_t prio = (flags >> 16) & 3u;
+    const bool rev = ((flags >> 21) & 1u) != 0;  // S4b's further rounds from the last lane pair (pfaai_run)
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
@@ -705,7 +706,10 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         if (has_i) {
             scatter8(acc_i, b, bh, okm);
             stamp(4);
-            for (int k = grpx + NGX; k < nt; k += NGX) {
+            // the rounds after the first: from the last lane pair down when
+            // flags bit 21 is set -- the first waves hold the G entries (S1-S3)
+            // and the first round's low task slots, the last waves idle in both
+            for (int k = rev ? 2 * NGX - 1 - grpx : grpx + NGX; k < nt; k += NGX) {
                 okm = issue2(k, nt, b, bh);
                 scatter8(acc_i, b, bh, okm);
             }
