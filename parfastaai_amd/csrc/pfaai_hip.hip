@@ -913,6 +913,16 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
         &per2, reinterpret_cast<const void*>(&k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>), NT, lds);
     auto* rec = static_cast<uint64_t*>(c->srec_a.p);
     const SrcFEnds src{Fp, Fg, D, (uint32_t)P, kb, g_lo, g_hi, 2 * n_kept < n_f};
+    // (PFAAI_SORT_DIRECT, diagnostics: both passes store each record from its
+    // registers, k_sort_scatter VAR bit 6, A/B of the LDS reorder)
+#ifdef PFAAI_DIAGNOSTICS
+    const bool sdirect = DIAG_ENV("PFAAI_SORT_DIRECT") != nullptr;
+    if (sdirect)
+        hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcFEnds, DstRecsEnds, 64>),
+                           dim3((int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per1))), dim3(NT), lds, s,
+                           src, DstRecsEnds{rec, kb, DB}, n_f, ntiles, 0, mask1, hist, gsum, base, tctr);
+    else
+#endif
     hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcFEnds, DstRecsEnds>),
                        dim3((int)std::min<int64_t>(ntiles, (int64_t)cus * std::max(1, per1))), dim3(NT), lds, s, src,
                        DstRecsEnds{rec, kb, DB}, n_f, ntiles, 0, mask1, hist, gsum, base, tctr);
@@ -923,6 +933,14 @@ int gpos_ends_passes(pfaai_ctx* c, int64_t n_f, int kb, int32_t g_lo, int32_t g_
         hipLaunchKernelGGL((k_sort_hist<DB, NT, SrcRecs>), dim3(nt2), dim3(NT), 0, s, src2, n_kept, 0, mask2, hist);
         hipLaunchKernelGGL((k_sort_grp<DB>), dim3(ng2), dim3(kSortThreads), 0, s, hist, nt2, gsum);
         hipLaunchKernelGGL((k_sort_top<DB>), dim3(1), dim3(kSortThreads), 0, s, gsum, ng2, base, tctr);
+#ifdef PFAAI_DIAGNOSTICS
+        if (sdirect)
+            hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds, 64>),
+                               dim3((int)std::min<int64_t>(nt2, (int64_t)cus * std::max(1, per2))), dim3(NT), lds, s,
+                               src2, DstGposEnds{static_cast<uint2*>(c->G_pe.p) + gbase, hb}, n_kept, nt2, 0, mask2,
+                               hist, gsum, base, tctr);
+        else
+#endif
         hipLaunchKernelGGL((k_sort_scatter<DB, NT, kSortPF, SrcRecs, DstGposEnds>),
                            dim3((int)std::min<int64_t>(nt2, (int64_t)cus * std::max(1, per2))), dim3(NT), lds, s, src2,
                            DstGposEnds{static_cast<uint2*>(c->G_pe.p) + gbase, hb},
@@ -1725,6 +1743,10 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     {  // k_rows_pl's S5 entry order (flags bits 18-20; pfaai_rows_pl.hpp): default 2, PFAAI_PL_STAG overrides (A/B)
         const char* sg = DIAG_ENV("PFAAI_PL_STAG");
         flags = (flags & ~(7u << 18)) | (uint32_t)((sg ? atoi(sg) : kPlStag) & 7) << 18;
+    }
+    {  // k_rows_pl's further member rounds from the last lane pair (flags bit 21): default kPlRev, PFAAI_PL_REV overrides (A/B)
+        const char* rv = DIAG_ENV("PFAAI_PL_REV");
+        flags = (flags & ~(1u << 21)) | (uint32_t)((rv ? atoi(rv) : kPlRev) & 1) << 21;
     }
     // k_rows_pl wave priorities: bit 0 raises the load-issue stages above other
     // waves' fp64 normalisation, bit 1 the scatter rounds (3: 11.52 -> 11.33

@@ -775,7 +775,7 @@ constexpr int sort_scatter_wpe() { return NT == 512 ? 4 : 1; }
 // PF: the next tile's records and digit bases are loaded while this tile is
 // ranked and written (16 + BPT VGPRs live across the tile)
 // VAR (diagnostics A/B, 0 in the product): bit 0 round-robin tile order,
-// bit 3 no global stores
+// bit 6 direct stores without the LDS reorder, bit 3 no global stores
 // (ablation), bit 4 ordinary (temporal) record loads, bit 5 a static tile
 // stride instead of the per-XCD tile counters (tctr[8], zeroed by k_sort_top)
 template <int DB, int NT, bool PF, class Src, class Dst, int VAR = 0>
@@ -997,6 +997,33 @@ __global__ __launch_bounds__(NT, sort_scatter_wpe<NT>()) void k_sort_scatter(
             }
             tot[q] = run;
             mine += run;
+        }
+        if constexpr ((VAR & 64) != 0) {
+            // direct stores (diagnostics A/B): each record from its registers
+            // to gbase[d] + (its rank among the tile's records of digit d) --
+            // no digit totals scan, no LDS reorder, 8-B stores spread over
+            // the tile's digit runs instead of one contiguous tile
+            (void)tot;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kSortItems; ++k) {
+                const uint32_t d = sort_digit(rec[k], shift, mask);
+                const uint32_t pos = gbase[d] + cnt[wid * BINS + d] + lr[k];
+                const bool ok = k < kact && t0 + (wid * kSortItems + k) * 64 + lane < n && src.keep(rec[k]);
+                if ((VAR & 8) == 0 && ok) hsum += dst.store(pos, rec[k], dst.fetch(pos, rec[k]), t0);
+            }
+            __syncthreads();  // the counters and bases are rewritten by the next tile
+            if constexpr (PF) {
+#pragma unroll
+                for (int k = 0; k < kSortItems; ++k) rec[k] = nrec[k];
+#pragma unroll
+                for (int q = 0; q < BPT; ++q) gb[q] = ngb[q];
+            } else {
+                tnext = next_tile(tile);
+                fetch_tile(tnext < tend ? tnext : ntiles, rec, gb);
+            }
+            tile = tnext;
+            continue;
         }
         uint32_t inc = mine;
 #pragma unroll

@@ -73,7 +73,7 @@ def test_product_does_not_import_oracle():
 AB_SWITCHES = (b"PFAAI_ROWS_KERNEL", b"PFAAI_XCD_CHUNK", b"PFAAI_PL_PRIO", b"PFAAI_PL_LAUNCH_COLS",
                b"PFAAI_PL_WINDOWS", b"PFAAI_BLK_THREADS", b"PFAAI_BLK_QT_SPLIT", b"PFAAI_BLK_END_TILE",
                b"PFAAI_BLK_END_U", b"PFAAI_PL_KWMAX", b"PFAAI_PL_BIGF", b"PFAAI_PL_NREG", b"PFAAI_PL_V",
-               b"PFAAI_PL_NOWK4", b"PFAAI_TRACE_COMPUTE", b"PFAAI_PL_T24", b"PFAAI_PL_STAG")
+               b"PFAAI_PL_NOWK4", b"PFAAI_TRACE_COMPUTE", b"PFAAI_PL_T24", b"PFAAI_PL_STAG", b"PFAAI_PL_REV", b"PFAAI_SORT_DIRECT")
 
 
 def test_release_library_ignores_diagnostic_switches():
