@@ -241,6 +241,13 @@ __device__ __forceinline__ void pl_scatter4_code(uint4 c, uint32_t m, uint32_t b
 #undef PL_SLOT
 }
 
+// S5's read of a finished counter word, which also clears it for the protein
+// two iterations on: one ds_wrxchg_rtn_b32 (exchange with 0) instead of a
+// read and, for a nonzero word, a second LDS store
+__device__ __forceinline__ uint32_t pl_take(uint32_t* w) {
+    return __hip_atomic_exchange(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // CLK (diagnostics, PFAAI_PL_CLK): every wave of the first kClkBlocks
 // workgroups sums the shader-clock time of each stage of the protein loop
 // into clk[(block * (NT / 64) + wave) * 8 + stage] (pfaai_debug_clocks,
@@ -571,9 +578,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             for (int k = 0; k < KW; ++k) {
                 if (WK == 3 && wbase + k * NT >= ncw) break;
                 const int32_t w = tid + k * NT;
-                const uint32_t v = acc_p[w];
+                const uint32_t v = pl_take(acc_p + w);
                 if (v) {
-                    acc_p[w] = 0u;
                     const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                     if constexpr (!EV3) ev += (uint32_t)(c0 + c1);
                     n_add(k, v);
@@ -598,9 +604,8 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
             // forms the early stop spilled 6 VGPRs -- 100k streamed 613 -> 689 ms)
             if (WK == 3 && wbase + k * NT >= ncw) break;
             const int32_t w = tid + k * NT;
-            const uint32_t v = acc_p[w];
+            const uint32_t v = pl_take(acc_p + w);
             if (v) {
-                acc_p[w] = 0u;
                 const int32_t c0 = (int32_t)(v & 0xFFFFu), c1 = (int32_t)(v >> 16);
                 if constexpr (!EV3) ev += (uint32_t)(c0 + c1);
                 n_add(k, v);
