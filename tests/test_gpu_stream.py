@@ -326,3 +326,34 @@ def test_stream_tiles_switch_window_and_end_table(engine):
         b = np.arange(a + 1, n)
         k = n * a + b - (a + 2) * (a + 1) // 2
         assert np.array_equal(N[k], No[0, b]) and np.array_equal(S[k], So[0, b]), a
+
+
+@pytest.mark.parametrize("var", ["PFAAI_PL_T24", "PFAAI_PL_REV", "PFAAI_SORT_DIRECT"])
+def test_diagnostic_variants_equal_release_form(diag_engine, monkeypatch, var):
+    """The round-6 A/B variants of the diagnostics build compute what the
+    release form computes, S / N / AJI / |E| bit for bit, on an all-vs-all
+    windowed load and a query-vs-target one: 24-member span tasks
+    (PFAAI_PL_T24), the further member rounds from the last lane pair down
+    (PFAAI_PL_REV), the load sort's direct stores without the LDS reorder
+    (PFAAI_SORT_DIRECT: the load is repeated under it).  Their timings are in
+    profiles/r06/ab_t24.txt, ab_rev.txt and ab_sort_direct.txt."""
+    engine = diag_engine
+    if var == "PFAAI_SORT_DIRECT":  # the run-end sort: all-vs-all, both orientations, <= 20 480 genomes
+        pbs = (_all_problem(3000, 20, clade_size=25, n_random=1),)
+    else:
+        pbs = (_all_problem(21000, 3, clade_size=50, n_random=1),
+               qt_syn(dict(n_tgt=12000, n_qry=40, n_prot=4, clade_size=30, n_random=1), genome_major=True).problem())
+    for pb in pbs:
+        monkeypatch.delenv(var, raising=False)
+        engine.load(**pb)
+        a1, S1, N1 = engine.compute(0)
+        e1 = engine.stats()["n_events"]
+        monkeypatch.setenv(var, "1")
+        if var == "PFAAI_SORT_DIRECT":
+            engine.load(**pb)
+        a2, S2, N2 = engine.compute(0)
+        if var == "PFAAI_SORT_DIRECT":
+            assert engine.stats()["walk"] == "gpos", engine.stats()
+        assert engine.stats()["n_events"] == e1
+        assert np.array_equal(N1, N2) and np.array_equal(S1, S2) and np.array_equal(a1, a2)
+        monkeypatch.delenv(var, raising=False)
