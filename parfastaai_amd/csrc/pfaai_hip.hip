@@ -1901,6 +1901,12 @@ int pfaai_set_row_order(pfaai_ctx* c, const int32_t* genomes, int64_t n) {
     HIPCHK(c, hipDeviceSynchronize());  // no launch in flight still reads the old order
     HIPCHK(c, hipMemcpy(c->row_genome.p, order.data(), (size_t)ni * sizeof(int32_t), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->row_of.p, row_of.data(), (size_t)ni * sizeof(int32_t), hipMemcpyHostToDevice));
+    {  // the work-list sizes follow the rows (pfaai_debug_row_counts' sorted path)
+        std::vector<int64_t> fcount((size_t)ni, 0);
+        for (int64_t r = 0; r < c->n_rows; ++r)
+            fcount[(size_t)c->row_genome_h[(size_t)r]] = c->row_fprefix[r + 1] - c->row_fprefix[r];
+        for (int64_t r = 0; r < c->n_rows; ++r) c->row_fprefix[r + 1] = c->row_fprefix[r] + fcount[(size_t)order[(size_t)r]];
+    }
     c->row_genome_h.swap(order);
     c->order_n = n;
     c->order_in_pos = in_pos;

@@ -168,9 +168,12 @@ def test_cyclic_row_lists_assemble_to_the_whole_run(engine, n, world, group):
     got = [torch.full_like(x, -2) for x in ref]
     lists = cyclic_rows(rows, world, group)
     assert sorted(r for rl in lists for r in rl) == list(range(rows))
+    # the sorted-E counts of a list's middle row (pfaai_debug_row_counts) follow the list too
+    mid = {rl[len(rl) // 2]: engine.debug_row_counts(rl[len(rl) // 2], 30, n) for rl in lists}
     base = lambda a: n * a - a * (a + 1) // 2
     for rl in lists:
         engine.set_row_order(rl)
+        assert np.array_equal(engine.debug_row_counts(len(rl) // 2, 30, n), mid[rl[len(rl) // 2]])
         part = [torch.full_like(x, -3) for x in ref]
         engine.run(0, len(rl), _capi.FLAG_EMIT_JAC, *(x.data_ptr() for x in part), stream=st)
         torch.cuda.synchronize()
