@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 if [ "${WHICH:-c4}" = c4 ]; then
   CMD="python3 tools/gpu/qt_bench.py --steps 3 --check-rows 1"
 else
-  CMD="python3 tools/gpu/stream_bench.py --genomes 100000 --sinks noop --check-rows 0"
+  CMD="python3 tools/gpu/stream_bench.py --genomes 100000 --device-only"
 fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ks" -o run -- $CMD > "$OUT/ks.log" 2>&1 || { tail -20 "$OUT/ks.log"; exit 1; }
 i=0

@@ -10,6 +10,7 @@
 #   qt_rev / stream_rev / rev  the C4 / C5 / C3 (ab_rows) runs with PFAAI_PL_REV=1 (A/B of the round order)
 #   sortab     A/B of the load sort's variants (tools/gpu/ab_sort.py, diagnostics build)
 #   abprev     bench + C4 twice each, alternating this library and PREV (a saved earlier build)
+#   stream_dev the C5 row tiles by pfaai_run into device buffers, no D2H (the row kernels alone)
 #   stream_r05 the same against round 5's library
 #   bench      the bench line (bench.py --steps 20 --warmup 5, no CPU baseline)
 #   cyclic     one-GPU emulation of the 8-way split: contiguous vs block-cyclic (tools/gpu/shard_cyclic.py)
@@ -48,6 +49,7 @@ for step in ${STEPS:-suite}; do
               PFAAI_HIP_LIB=$L timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline none >> "$OUT/abprev_bench_$n.json" 2>> "$OUT/abprev.err" || exit 1
               PFAAI_HIP_LIB=$L timeout -k 10 300 python3 -u tools/gpu/qt_bench.py --steps 5 >> "$OUT/abprev_qt_$n.json" 2>> "$OUT/abprev.err" || exit 1
             done ;;
+    stream_dev) timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --device-only > "$OUT/stream_100k_device.json" 2> "$OUT/stream_dev.err" || exit 1 ;;
     stream_r05) PFAAI_HIP_LIB=$R05 timeout -k 10 600 python3 -u tools/gpu/stream_bench.py --genomes 100000 --sinks noop par > "$OUT/stream_100k_r05.json" 2> "$OUT/stream_r05.err" || exit 1 ;;
     bench) timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --cpu-baseline none > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1 ;;
     cyclic) timeout -k 10 400 python3 -u tools/gpu/shard_cyclic.py 10000 8 --reps 5 > "$OUT/shard_cyclic.txt" 2> "$OUT/shard_cyclic.err" || exit 1 ;;

@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--check-rows", type=int, default=2, help="rows re-checked against a pfaai_run of them")
     ap.add_argument("--sinks", nargs="+", default=["par"], choices=["noop", "copy", "par"])
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--device-only", action="store_true",
+                    help="the same row tiles by pfaai_run into two device buffers, no D2H: the row kernels "
+                         "alone (the profile command of C5 -- the stream's tile copies are blit kernels that "
+                         "share the CUs)")
     args = ap.parse_args()
     from concurrent.futures import ThreadPoolExecutor
     from parfastaai_amd import _capi, syn
@@ -78,6 +82,45 @@ def main():
                 last[0] = now
             return 0
         return fn
+
+    if args.device_only:
+        # row tiles of <= tile_pairs pairs, as pfaai_stream cuts them
+        cuts = [0]
+        while cuts[-1] < n_rows:
+            lo, hi = cuts[-1] + 1, n_rows
+            while lo < hi:  # the largest re whose span fits
+                mid = (lo + hi + 1) // 2
+                if eng.row_span(cuts[-1], mid)[1] <= args.tile_pairs:
+                    lo = mid
+                else:
+                    hi = mid - 1
+            cuts.append(lo)
+        bufs = [torch.empty(args.tile_pairs, dtype=torch.float64, device="cuda:0") for _ in range(2)]
+        st = torch.cuda.current_stream().cuda_stream
+        for rep in range(3):  # pass 0 builds the window tables and warms the clocks; pass 1 counts |E|; pass 2 is timed back to back
+            eng.timing(reset=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n_events = 0
+            for k in range(len(cuts) - 1):
+                f, c = eng.row_span(cuts[k], cuts[k + 1])
+                eng.run(cuts[k], cuts[k + 1], 0, bufs[k & 1].data_ptr() - f * 8, stream=st)
+                if rep == 1:  # (the event count is read after the run: a synchronising read per tile)
+                    torch.cuda.synchronize()
+                    n_events += eng.stats()["n_events"]
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            n_runs, ms_build, ms_rows = eng.timing(reset=True)
+            if rep == 1:
+                events = n_events
+        print(json.dumps({
+            "what": "C5 row tiles by pfaai_run into device buffers (no D2H): the row kernels alone",
+            "genomes": args.genomes, "proteins": args.prot, "F": n_f, "pairs": n_pairs, "events": events,
+            "tiles": len(cuts) - 1, "tile_pairs": args.tile_pairs, "wall_s": round(wall, 3),
+            "device_ms_rows": round(ms_rows, 2), "device_ms_build": round(ms_build, 2), "runs": n_runs,
+            "device_pairs_per_s": round(n_pairs / (ms_rows + ms_build) * 1e3, 1)}), flush=True)
+        eng.close()
+        return
 
     walls = {}
     for kind in args.sinks:
