@@ -47,7 +47,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-X
+E2E_PROFILE = "r06/final/e2e_c2.json"  # tools/gpu/e2e_c2.py's latest committed run (README quotes the same file)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "genome-pairs/sec (AJI matrix fill) + achieved HBM GB/s, 10k-genome all-vs-all"
 ROWS_KERNEL = ("pfaai::k_rows_pl (fused scatter + Jaccard + AJI; the wide rows as 1024-thread workgroups, the "
