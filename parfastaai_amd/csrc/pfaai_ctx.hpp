@@ -163,9 +163,6 @@ constexpr int64_t kMaxF = ((int64_t)1 << 32) - 64;
 constexpr int32_t kGposMaxIds = 20480;  // G_pos built for all-vs-all problems up to two row chunks wide
 
 enum RowsKernel { RK_PL = 0, RK_PL512 = 1, RK_FUSED = 2, RK_WORKLIST = 3 };
-constexpr int kPlStag = 2;
-// k_rows_pl's rounds after the first taken from the last lane pair down (flags bit 21)
-constexpr int kPlRev = 0;  // k_rows_pl's S5 entry order (pfaai_rows_pl.hpp, flags bits 18-20)
 
 // scalars buffer layout (u64 each)
 // SC_HF / SC_HG: the both-given load's membership sums over F (k_hash_f) and

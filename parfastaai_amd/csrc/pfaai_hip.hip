@@ -1753,7 +1753,7 @@ int pfaai_run(pfaai_ctx* c, int64_t rb, int64_t re, uint32_t flags, double* aji,
     // ms at 10k, tools/gpu/ab_rows.py); PFAAI_PL_PRIO=0..3 overrides (A/B)
     {
         const char* pr = DIAG_ENV("PFAAI_PL_PRIO");
-        flags = (flags & ~(3u << 16)) | (uint32_t)((pr ? atoi(pr) : 3) & 3) << 16;
+        flags = (flags & ~(3u << 16)) | (uint32_t)((pr ? atoi(pr) : kPlPrio) & 3) << 16;
     }
     if (c->pool_used >= 3 * 4096) {  // nobody reads the window: recycle it
         HIPCHK(c, hipStreamSynchronize(s));

@@ -59,6 +59,14 @@ constexpr int kPlEntries = 1024;   // G entries per (genome, protein) (host-chec
 constexpr int kPlTaskCap = 4096;   // u16 line tasks per protein stage: run slot | line << 10
 constexpr int kPlMaxLines = 63;    // runs with more lines go to the whole-workgroup walk
 constexpr uint16_t kPlNoTask = 0xFFFFu;
+// k_rows_pl's scheduling switches in flags (set by pfaai_run from these
+// defaults; PFAAI_PL_PRIO / _STAG / _REV override them in the diagnostics build):
+// bits 16-17 wave priorities of the load-issue stages / scatter rounds,
+// bits 18-20 the S5 entry order, bit 21 the further member rounds from the
+// last lane pair down
+constexpr int kPlPrio = 3;
+constexpr int kPlStag = 2;
+constexpr int kPlRev = 0;
 // k_rows_pl's column selection (its abs_chunk argument) besides a fixed
 // window index >= 0: per-row chunks, the row's diagonal window, or a grid
 // of windows over blockIdx.y starting at window kWinGrid0 - abs_chunk
@@ -349,8 +357,13 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
     const int32_t ncw = (whi - cc0 + 1) >> 1;
     const bool compat = (V & 64) != 0 ? false : (flags & 1u) != 0;  // V 64: launched only without REF_COMPAT
     const uint32_t min_len = win >= 0 ? 0u : 1u;  // window sub-runs: one member may be a partner
+    // the scheduling switches of flags bits 16-21 (pfaai_run sets them, kPl*
+    // defaults above), read at run time in both builds: compiling the release
+    // defaults in measured slower (C3 6.80 -> 6.84 ms, C4 rows 6.58 -> 6.66 ms,
+    // profiles/r06/ab_const_flags.txt -- a different code layout of the loop)
     const uint32_t prio = (flags >> 16) & 3u;
-    const bool rev = ((flags >> 21) & 1u) != 0;  // S4b's further rounds from the last lane pair (pfaai_run)
+    const bool rev = ((flags >> 21) & 1u) != 0;  // S4b's further rounds from the last lane pair
+    const uint32_t stag = (flags >> 18) & 7u;   // S5 entry order
     const int P = d.n_prot;
     uint32_t* acc = pl_smem;
     uint32_t* goff = pl_smem + 2 * W;
@@ -662,7 +675,7 @@ __global__ __launch_bounds__(NT, WPE) void k_rows_pl(Dev d, int64_t row_begin, i
         // 7.96; 3 / 5 the second half sleeping 128 / 512 cycles first 8.09 /
         // 8.29; 4 waves 0-3 at priority 3: 8.24.  (6: the first half at 0 and
         // the second at 2; 7: waves 0-3 at 0.)
-        if (const uint32_t sg = (flags >> 18) & 7u) {
+        if (const uint32_t sg = stag) {
             const int wv = tid >> 6;
             const bool late = wv >= NT / 128;
             if (sg == 2) {
